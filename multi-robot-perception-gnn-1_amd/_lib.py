@@ -1,0 +1,80 @@
+"""ctypes binding of the HIP C-ABI library ``lib/libmrp_gnn.so`` (declared in ``include/mrp_gnn.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or ``python -m mrp_gnn_amd.build``).
+There is deliberately no CPU fallback: if the shared object is missing, every compute call
+raises.  torch is imported first so that the process already holds torch's HIP runtime
+(soname ``libamdhip64.so.7``) and the library binds to that same runtime, making torch's
+streams and device pointers valid inside it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be loaded before the HIP library, see module docstring)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
+
+#: Every symbol ``include/mrp_gnn.h`` declares.
+EXPORTED_SYMBOLS = (
+    "mrp_film_mean_fwd",
+    "mrp_film_mean_bwd",
+    "mrp_abi_version",
+    "mrp_error_string",
+)
+ABI_VERSION = 1
+MAX_NODES = 16
+
+MODE_FILM_MEAN = 0
+MODE_FILM_SUM = 1
+MODE_COPY_MEAN = 2
+MODES = {"film_mean": MODE_FILM_MEAN, "film_sum": MODE_FILM_SUM, "copy_mean": MODE_COPY_MEAN}
+
+_lock = threading.Lock()
+_lib = None
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    graph = [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32]  # indptr..mode
+    lib.mrp_film_mean_fwd.argtypes = [_P, _I64, _P] + graph + [_P, _I64, _P]
+    lib.mrp_film_mean_fwd.restype = ctypes.c_int
+    lib.mrp_film_mean_bwd.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _P]
+    lib.mrp_film_mean_bwd.restype = ctypes.c_int
+    lib.mrp_abi_version.argtypes = []
+    lib.mrp_abi_version.restype = ctypes.c_int
+    lib.mrp_error_string.argtypes = [ctypes.c_int]
+    lib.mrp_error_string.restype = ctypes.c_char_p
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raise if it has not been built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.isfile(path):
+            raise RuntimeError(
+                f"mrp_gnn: HIP library not found at {path}. Build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950). "
+                "There is no CPU fallback for the aggregation kernels."
+            )
+        lib = ctypes.CDLL(path)
+        _declare(lib)
+        got = lib.mrp_abi_version()
+        if got != ABI_VERSION:
+            raise RuntimeError(f"mrp_gnn: ABI version mismatch: library {got}, bindings {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        msg = load_library().mrp_error_string(code)
+        text = msg.decode() if msg else "unknown error"
+        raise RuntimeError(f"mrp_gnn: {what} failed with HIP error {code}: {text}")

@@ -1,0 +1,155 @@
+"""FiLM-mean message passing on the GPU: the replacement for ``g.update_all(edge_udf, node_udf)``.
+
+Reference semantics (``dgl/model/models.py:207-211,223``)::
+
+    m_e   = gamma_e * x[src(e)] + beta_e        # edge_udf, gamma/beta broadcast over H x W
+    out_v = mean_{e: dst(e) = v} m_e            # node_udf over v's mailbox; zeros if deg v = 0
+
+``gb`` is the edge encoder's sigmoid output viewed ``(E, C, 2)`` (gamma = ``[..., 0]``,
+beta = ``[..., 1]``, ``models.py:154-155``) and is read in place, never split or copied.
+
+Everything here dispatches to the HIP library through its C ABI; a CPU tensor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+from .graph import GraphCSR
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def node_stride(t: torch.Tensor) -> Optional[int]:
+    """Node stride of a (N, C, H, W) fp32 tensor whose per-node C*H*W block is contiguous,
+    else None (then the caller makes it contiguous)."""
+    if t.dim() != 4 or t.dtype != torch.float32:
+        return None
+    n, c, h, w = t.shape
+    if n == 0 or c * h * w == 0:
+        return c * h * w
+    s = t.stride()
+    if (w == 1 or s[3] == 1) and (h == 1 or s[2] == w) and (c == 1 or s[1] == h * w) and (n == 1 or s[0] >= c * h * w):
+        return s[0] if n > 1 else c * h * w
+    return None
+
+
+def _as_node_major(t: torch.Tensor):
+    s = node_stride(t)
+    if s is None:
+        t = t.contiguous()
+        s = t.shape[1] * t.shape[2] * t.shape[3]
+    return t, s
+
+
+def _require_device(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                "mrp_gnn: the FiLM-mean aggregation runs only on the GPU (HIP, gfx950); got a "
+                f"{t.device} tensor. There is no CPU fallback.")
+
+
+def _stream(dev: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def film_mean_forward_into(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode: int,
+                           out: torch.Tensor) -> torch.Tensor:
+    """Run the forward kernel into ``out`` (N, C, H, W) — which may be a strided view such as
+    the second half of a ``torch.cat((h, g_h), 1)`` buffer.  No autograd."""
+    _require_device(x, out)
+    n, C, H, W = x.shape
+    x, xs = _as_node_major(x)
+    os_ = node_stride(out)
+    if os_ is None or tuple(out.shape) != (n, C, H, W):
+        raise ValueError("out must be (N, C, H, W) fp32 with a contiguous C*H*W block per node")
+    if mode != _lib.MODE_COPY_MEAN:
+        if gb is None:
+            raise ValueError("gamma/beta tensor required for FiLM modes")
+        gb = gb.reshape(csr.num_edges, C, 2)
+        if not gb.is_contiguous() or gb.dtype != torch.float32:
+            gb = gb.contiguous().float()
+        _require_device(gb)
+    else:
+        gb = None
+    if n != csr.num_nodes:
+        raise ValueError(f"x has {n} nodes, graph has {csr.num_nodes}")
+    lib = _lib.load_library()
+    with torch.cuda.device(x.device):
+        code = lib.mrp_film_mean_fwd(
+            _ptr(x), xs, _ptr(gb), _ptr(csr.indptr), _ptr(csr.src), _ptr(csr.eid), _ptr(csr.graph_off),
+            csr.num_graphs, csr.max_nodes, csr.num_nodes, csr.num_edges, C, H * W, mode,
+            _ptr(out), os_, _stream(x.device))
+    _lib.check(code, "mrp_film_mean_fwd")
+    return out
+
+
+def film_mean_backward(grad_out: torch.Tensor, x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR,
+                       mode: int, need_dx: bool, need_dgb: bool):
+    """(grad_x or None, grad_gb (E, C, 2) or None) for the forward above."""
+    _require_device(grad_out, x)
+    n, C, H, W = x.shape
+    grad_out, gs = _as_node_major(grad_out)
+    dx = torch.empty((n, C, H, W), device=x.device, dtype=torch.float32) if need_dx else None
+    dgb = torch.empty((csr.num_edges, C, 2), device=x.device, dtype=torch.float32) if need_dgb else None
+    xs = 0
+    if need_dgb and mode != _lib.MODE_COPY_MEAN:
+        x, xs = _as_node_major(x)
+    if gb is not None:
+        gb = gb.reshape(csr.num_edges, C, 2)
+        if not gb.is_contiguous():
+            gb = gb.contiguous()
+    lib = _lib.load_library()
+    with torch.cuda.device(x.device):
+        code = lib.mrp_film_mean_bwd(
+            _ptr(grad_out), gs, _ptr(x), xs, _ptr(gb), _ptr(csr.indptr), _ptr(csr.src), _ptr(csr.eid),
+            _ptr(csr.graph_off), csr.num_graphs, csr.max_nodes, csr.num_nodes, csr.num_edges, C, H * W, mode,
+            _ptr(dx), (C * H * W) if dx is not None else 0, _ptr(dgb), _stream(x.device))
+    _lib.check(code, "mrp_film_mean_bwd")
+    return dx, dgb
+
+
+class FilmMeanFunction(torch.autograd.Function):
+    """Autograd wrapper: forward = ``mrp_film_mean_fwd``, backward = ``mrp_film_mean_bwd``."""
+
+    @staticmethod
+    def forward(ctx, x, gb, csr: GraphCSR, mode: int):
+        out = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+        film_mean_forward_into(x, gb, csr, mode, out)
+        ctx.save_for_backward(x, gb)
+        ctx.csr = csr
+        ctx.mode = mode
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        x, gb = ctx.saved_tensors
+        need_dx = ctx.needs_input_grad[0]
+        need_dgb = gb is not None and ctx.needs_input_grad[1]
+        dx, dgb = film_mean_backward(grad_out, x, gb, ctx.csr, ctx.mode, need_dx, need_dgb)
+        if dgb is not None:
+            dgb = dgb.view(gb.shape)
+        return dx, dgb, None, None
+
+
+def film_mean(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="film_mean") -> torch.Tensor:
+    """``mean_e(gamma_e * x_src + beta_e)`` per destination node (see module docstring).
+
+    x: (N, C, H, W) fp32 on a ROCm device; gb: (E, 2C) or (E, C, 2) interleaved gamma/beta
+    (ignored for ``mode='copy_mean'``); csr: ``RobotGraph.csr(device)``.
+    """
+    m = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
+    if x.dim() != 4:
+        raise ValueError(f"node features must be (N, C, H, W), got {tuple(x.shape)}")
+    if x.dtype != torch.float32:
+        raise TypeError("node features must be float32 (the reference path is fp32)")
+    _require_device(x)
+    if m == _lib.MODE_COPY_MEAN:
+        gb = None
+    return FilmMeanFunction.apply(x, gb, csr, m)

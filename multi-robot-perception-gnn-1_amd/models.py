@@ -1,0 +1,153 @@
+"""Drop-in model classes for the GCN hot path, with the reference's API and ``state_dict`` keys.
+
+Mirrors ``dgl/model/models.py``:
+
+* :class:`edge_encoder`  — ``models.py:142-155``: ``Linear(9,C) -> ReLU -> Linear(C,2C) -> Sigmoid``;
+  keys ``layers.0.weight``, ``layers.0.bias``, ``layers.2.weight``, ``layers.2.bias``.
+* :class:`GCN`           — ``models.py:213-226``: ``forward(g)`` (the reference call, ``models.py:181``)
+  and ``forward(g, feats)`` (the north-star signature).  Aggregation runs in the HIP kernel.
+* :class:`GCNBlock`      — the GCN stacking of ``multi_view_dgl_model.forward`` (``models.py:180-189``):
+  ``gcn1 -> cat -> [conv1] -> [gcn2 -> cat -> conv2]``, keys ``gcn1.*``, ``conv1.*``, ``gcn2.*``, ``conv2.*``.
+* :class:`multi_view_dgl_model` — ``models.py:157-205`` with the CNN encoder/decoder supplied by the
+  caller (they are torchvision/dense-conv code outside the hot path), so a reference
+  ``encoder``/``decoder`` instance can be plugged in unchanged.
+
+Semantics switch ``opt.gcn_return``:
+
+* ``'aggregate'`` (default): return the FiLM-mean aggregate — what ``update_all`` computes and
+  what the scratch variants return (``dgl/model/dgl_models.py:61,127,189``).
+* ``'input'``: bit-faithful to ``models.py:226``, which returns ``g.ndata['image']`` (the input)
+  because ``node_udf`` writes ``'images'``; the aggregate is then dead work and is skipped.
+
+``opt.gcn_mode``: ``'film_mean'`` (default, ``models.py:223``), ``'copy_mean'`` (the commented-out
+``fn.copy_u`` variant, ``models.py:225``), ``'film_sum'``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .aggregate import film_mean
+
+
+class edge_encoder(nn.Module):  # noqa: N801  (reference class name)
+    """FiLM parameter generator, ``dgl/model/models.py:142-155``."""
+
+    def __init__(self, layers_dim):
+        super().__init__()
+        self.layers_dim = layers_dim
+        self.layers = nn.Sequential(
+            nn.Linear(9, layers_dim[0]),
+            nn.ReLU(),
+            nn.Linear(layers_dim[0], layers_dim[1] * 2),
+            nn.Sigmoid(),
+        )
+
+    def film_params(self, edge: torch.Tensor) -> torch.Tensor:
+        """Interleaved gamma/beta, (E, C, 2): the tensor the kernel reads in place."""
+        return self.layers(edge.float()).view(-1, self.layers_dim[1], 2)
+
+    def forward(self, edge: torch.Tensor):
+        """Reference return value: gamma, beta as (E, C, 1, 1) views (``models.py:152-155``)."""
+        gb = self.film_params(edge)
+        return gb[:, :, 0].unsqueeze(-1).unsqueeze(-1), gb[:, :, 1].unsqueeze(-1).unsqueeze(-1)
+
+
+def _opt(opt, name, default):
+    return getattr(opt, name, default) if opt is not None else default
+
+
+class GCN(nn.Module):
+    """FiLM-mean graph convolution over per-frame robot graphs, ``dgl/model/models.py:213-226``."""
+
+    def __init__(self, opt):
+        super().__init__()
+        self.opt = opt
+        self.edge_encoder = edge_encoder(layers_dim=[opt.feature_dim, opt.feature_dim])
+
+    def forward(self, g, feats: torch.Tensor = None) -> torch.Tensor:
+        x = g.ndata["image"] if feats is None else feats
+        if _opt(self.opt, "gcn_return", "aggregate") == "input":
+            return x  # models.py:226 returns the input; update_all's result is never read
+        mode = _opt(self.opt, "gcn_mode", "film_mean")
+        gb = None
+        if mode != "copy_mean":
+            gb = self.edge_encoder.film_params(g.edata["pose"])
+        return film_mean(x, gb, g.csr(x.device), mode)
+
+
+class GCNBlock(nn.Module):
+    """GCN stacking of ``multi_view_dgl_model`` (``dgl/model/models.py:162-171,180-189``)."""
+
+    def __init__(self, opt):
+        super().__init__()
+        self.opt = opt
+        self.gcn1 = GCN(opt)
+        if opt.compress_gcn:
+            self.conv1 = nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1)
+        if opt.multi_gcn:
+            assert opt.compress_gcn  # models.py:169
+            self.gcn2 = GCN(opt)
+            self.conv2 = nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1)
+
+    def forward(self, g, h: torch.Tensor) -> torch.Tensor:
+        g_h = self.gcn1(g, h)
+        h = torch.cat((h, g_h), dim=1)
+        if self.opt.compress_gcn:
+            h = self.conv1(h)
+        if self.opt.multi_gcn:
+            g_h = self.gcn2(g, h)
+            h = torch.cat((h, g_h), dim=1)
+            h = self.conv2(h)
+        return h
+
+
+class multi_view_dgl_model(nn.Module):  # noqa: N801  (reference class name)
+    """``dgl/model/models.py:157-205`` with caller-supplied CNN ``encoder``/``decoder``.
+
+    ``encoder(images (B, N, 3, S, S)) -> list of feature maps`` (last one used) and
+    ``decoder(h) -> prediction`` follow the reference modules' call signatures; with
+    ``encoder=None`` the node features in ``g.ndata['image']`` are taken to be feature maps
+    already (the synthetic benchmark setting).
+    """
+
+    def __init__(self, opt, encoder: nn.Module = None, decoder: nn.Module = None):
+        super().__init__()
+        self.opt = opt
+        if encoder is not None:
+            self.encoder = encoder
+        self.gcn1 = GCN(opt)
+        if opt.compress_gcn:
+            self.conv1 = nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1)
+        if decoder is not None:
+            self.decoder = decoder
+        if opt.multi_gcn:
+            assert opt.compress_gcn
+            self.gcn2 = GCN(opt)
+            self.conv2 = nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1)
+
+    def features(self, g) -> torch.Tensor:
+        """Encoder output per node, (B*N, C, h, w) (``models.py:175-179``)."""
+        image = g.ndata["image"]
+        if not hasattr(self, "encoder"):
+            return image
+        image = image.view(-1, self.opt.camera_num, 3, self.opt.image_size, self.opt.image_size)
+        h = self.encoder(image)[-1]
+        return h.view(-1, h.size()[-3], h.size()[-2], h.size()[-1])
+
+    def forward(self, g):
+        with g.local_scope():
+            h = self.features(g)
+            g.ndata["image"] = h
+            g_h = self.gcn1(g)
+            h = torch.cat((h, g_h), dim=1)
+            if self.opt.compress_gcn:
+                h = self.conv1(h)
+            if self.opt.multi_gcn:
+                g.ndata["image"] = h
+                g_h = self.gcn2(g)
+                h = torch.cat((h, g_h), dim=1)
+                h = self.conv2(h)
+            if not hasattr(self, "decoder"):
+                return h
+            return self.decoder(h)

@@ -1,0 +1,82 @@
+"""CPU: the C-ABI library loads and exports every symbol include/*.h declares; argument
+validation and no-op paths (no compute launch, so no GPU needed); the product has no CPU fallback."""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+import mrp_gnn_amd as m
+from mrp_gnn_amd import _lib
+from conftest import ROOT
+
+HIP_INVALID_VALUE = 1
+
+
+def declared_symbols():
+    syms = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = open(h).read()
+        syms |= set(re.findall(r"^\s*(?:int|const char\*|void)\s+(mrp_\w+)\s*\(", text, re.M))
+    return syms
+
+
+def test_header_declares_expected_symbols():
+    assert declared_symbols() == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = m.load_library()
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (mrp_\w+)$", out, re.M))
+    assert declared_symbols() <= exported
+
+
+def test_library_targets_gfx950_only():
+    data = open(_lib.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa-+(gfx\w+)", data))
+    assert targets == {b"gfx950"}
+
+
+def test_abi_version_and_errors():
+    lib = m.load_library()
+    assert lib.mrp_abi_version() == _lib.ABI_VERSION
+    assert b"invalid" in lib.mrp_error_string(HIP_INVALID_VALUE).lower()
+
+
+def _fwd(lib, **kw):
+    a = dict(x=None, xs=0, gb=None, indptr=None, src=None, eid=None, goff=None, B=0, maxn=0, Nt=0, E=0,
+             C=0, P=0, mode=0, out=None, os=0, stream=None)
+    a.update(kw)
+    return lib.mrp_film_mean_fwd(a["x"], a["xs"], a["gb"], a["indptr"], a["src"], a["eid"], a["goff"], a["B"],
+                                 a["maxn"], a["Nt"], a["E"], a["C"], a["P"], a["mode"], a["out"], a["os"],
+                                 a["stream"])
+
+
+def test_argument_validation_without_launch():
+    lib = m.load_library()
+    dummy = ctypes.c_void_p(16)
+    assert _fwd(lib) == 0  # empty batch: no-op
+    assert _fwd(lib, maxn=17, B=1, Nt=1, goff=dummy, indptr=dummy) == HIP_INVALID_VALUE  # > MRP_MAX_NODES
+    assert _fwd(lib, mode=3) == HIP_INVALID_VALUE
+    assert _fwd(lib, C=-1) == HIP_INVALID_VALUE
+    # more nodes than num_graphs * max_nodes can hold
+    assert _fwd(lib, B=1, maxn=2, Nt=3, goff=dummy, indptr=dummy) == HIP_INVALID_VALUE
+    # stride smaller than a node's C*P block
+    assert _fwd(lib, B=1, maxn=2, Nt=2, goff=dummy, indptr=dummy, C=2, P=4, x=dummy, out=dummy, xs=7, os=8,
+                mode=2) == HIP_INVALID_VALUE
+    # bwd: nothing requested -> no-op
+    assert lib.mrp_film_mean_bwd(None, 0, None, 0, None, None, None, None, None, 0, 0, 0, 0, 0, 0, 0, None, 0,
+                                 None, None) == 0
+
+
+def test_no_cpu_fallback():
+    g = m.complete_graph(3)
+    x = torch.randn(3, 2, 4, 4)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m.film_mean(x, torch.rand(6, 2, 2), g.csr("cpu"))
