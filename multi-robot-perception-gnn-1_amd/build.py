@@ -34,7 +34,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     tmp = OUT + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-mcode-object-version=5",
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-mcode-object-version=5", "-ffp-contract=off",
            "-Wno-pass-failed", "-I", os.path.join(REPO, "include"), "-o", tmp] + SOURCES
     if verbose:
         print("[mrp_gnn build]", " ".join(cmd), flush=True)
