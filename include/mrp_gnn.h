@@ -46,6 +46,16 @@ extern "C" {
 
 #define MRP_MAX_NODES 16
 
+/* Graph kinds.  MRP_GRAPH_COMPLETE is the reference's only topology (dgl/dataloader.py:88-95):
+ * every graph has exactly max_nodes nodes, edges are all ordered pairs u != v, numbered graph by
+ * graph in i-major order (edge u->v of graph b is b*n*(n-1) + u*(n-1) + (v < u ? v : v-1)), and
+ * node ids are graph by graph.  indptr/src/eid/graph_off are then not read (may be NULL).
+ * MRP_GRAPH_CSR is any batch of disjoint graphs described by the CSR arrays. */
+enum mrp_graph_kind {
+    MRP_GRAPH_CSR = 0,
+    MRP_GRAPH_COMPLETE = 1
+};
+
 /* Aggregation modes (the reference's UDF variants). */
 enum mrp_agg_mode {
     MRP_AGG_FILM_MEAN = 0, /* mean_e(gamma_e*x_u + beta_e): models.py:207-211          */
@@ -65,13 +75,14 @@ enum mrp_agg_mode {
  *   src, eid   (num_edges) int32
  *   graph_off  (num_graphs + 1) int32 node offsets of the batched graphs
  *   max_nodes  max_b (graph_off[b+1] - graph_off[b]), 0..MRP_MAX_NODES (host-known)
+ *   graph_kind MRP_GRAPH_CSR or MRP_GRAPH_COMPLETE (see enum mrp_graph_kind)
  *   out        (num_nodes, C, P) fp32, node stride out_node_stride (elements)
  */
 int mrp_film_mean_fwd(const float* x, int64_t x_node_stride,
                       const float* gb,
                       const int32_t* indptr, const int32_t* src, const int32_t* eid,
                       const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes,
-                      int32_t num_nodes, int32_t num_edges,
+                      int32_t graph_kind, int32_t num_nodes, int32_t num_edges,
                       int32_t C, int32_t P, int32_t mode,
                       float* out, int64_t out_node_stride,
                       void* stream);
@@ -94,7 +105,7 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride,
                       const float* gb,
                       const int32_t* indptr, const int32_t* src, const int32_t* eid,
                       const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes,
-                      int32_t num_nodes, int32_t num_edges,
+                      int32_t graph_kind, int32_t num_nodes, int32_t num_edges,
                       int32_t C, int32_t P, int32_t mode,
                       float* grad_x, int64_t gx_node_stride,
                       float* grad_gb,

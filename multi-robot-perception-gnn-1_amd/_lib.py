@@ -24,12 +24,14 @@ EXPORTED_SYMBOLS = (
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_NODES = 16
 
 MODE_FILM_MEAN = 0
 MODE_FILM_SUM = 1
 MODE_COPY_MEAN = 2
+GRAPH_CSR = 0
+GRAPH_COMPLETE = 1
 MODES = {"film_mean": MODE_FILM_MEAN, "film_sum": MODE_FILM_SUM, "copy_mean": MODE_COPY_MEAN}
 
 _lock = threading.Lock()
@@ -41,7 +43,7 @@ _I64 = ctypes.c_int64
 
 
 def _declare(lib: ctypes.CDLL) -> None:
-    graph = [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32]  # indptr..mode
+    graph = [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32]  # indptr..mode
     lib.mrp_film_mean_fwd.argtypes = [_P, _I64, _P] + graph + [_P, _I64, _P]
     lib.mrp_film_mean_fwd.restype = ctypes.c_int
     lib.mrp_film_mean_bwd.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _P]

@@ -84,7 +84,7 @@ def film_mean_forward_into(x: torch.Tensor, gb: Optional[torch.Tensor], csr: Gra
     with torch.cuda.device(x.device):
         code = lib.mrp_film_mean_fwd(
             _ptr(x), xs, _ptr(gb), _ptr(csr.indptr), _ptr(csr.src), _ptr(csr.eid), _ptr(csr.graph_off),
-            csr.num_graphs, csr.max_nodes, csr.num_nodes, csr.num_edges, C, H * W, mode,
+            csr.num_graphs, csr.max_nodes, csr.graph_kind, csr.num_nodes, csr.num_edges, C, H * W, mode,
             _ptr(out), os_, _stream(x.device))
     _lib.check(code, "mrp_film_mean_fwd")
     return out
@@ -109,7 +109,8 @@ def film_mean_backward(grad_out: torch.Tensor, x: torch.Tensor, gb: Optional[tor
     with torch.cuda.device(x.device):
         code = lib.mrp_film_mean_bwd(
             _ptr(grad_out), gs, _ptr(x), xs, _ptr(gb), _ptr(csr.indptr), _ptr(csr.src), _ptr(csr.eid),
-            _ptr(csr.graph_off), csr.num_graphs, csr.max_nodes, csr.num_nodes, csr.num_edges, C, H * W, mode,
+            _ptr(csr.graph_off), csr.num_graphs, csr.max_nodes, csr.graph_kind, csr.num_nodes, csr.num_edges, C,
+            H * W, mode,
             _ptr(dx), (C * H * W) if dx is not None else 0, _ptr(dgb), _stream(x.device))
     _lib.check(code, "mrp_film_mean_bwd")
     return dx, dgb

@@ -7,21 +7,27 @@
 //     node_udf: out_v = mailbox['m'].mean(1)           :207-208
 //
 // Design:
-//   * One workgroup = one per-frame graph (<= 16 nodes) x a block of channels.
-//     Its prologue turns the graph's in-edges and the interleaved (E, C, 2)
-//     gamma/beta rows into dense per-channel N x N weight tiles in LDS.
-//   * The main loop is one coalesced HBM sweep over the channel planes: every lane
-//     owns a 16-byte slice p of one channel plane, loads that slice of all N source
-//     nodes once (N x dwordx4), and emits all N destination slices from registers.
-//     Each source map is therefore read exactly once, instead of deg(v) times plus
-//     the E x C x H x W message/mailbox tensors DGL materialises.
-//   * The forward keeps the reference's rounding order exactly for edges listed in
-//     ascending source order (complete i-major graphs, our kNN builder):
+//   * One workgroup = one per-frame graph (<= 16 nodes) x a block of channels.  Its prologue
+//     turns the graph's edges and the interleaved (E, C, 2) gamma/beta rows into dense
+//     per-channel N x N weight tiles in LDS.  Two graph kinds:
+//       - COMPLETE: the reference's only topology (dgl/dataloader.py:88-95), every graph with
+//         exactly NT nodes, edges numbered graph by graph i-major: edge ids are arithmetic, one
+//         gamma/beta load per LDS slot, and the neighbour mask (u != v) is compile-time;
+//       - CSR: any graph (k-NN, ragged batches, multi-edges, self-loops): in-edges walked from
+//         the CSR-by-destination arrays.
+//   * The main loop is one coalesced HBM sweep over the channel planes: every lane owns a
+//     16-byte slice of one channel plane, loads that slice of all N source nodes once
+//     (N x dwordx4, nontemporal: read once), and emits all N destination slices from registers
+//     (nontemporal stores).  Each source map is read exactly once, instead of deg(v) times plus
+//     the E x C x H x W message and mailbox tensors DGL materialises.  The first slice's loads are
+//     issued before the prologue's LDS writes so the weight build hides under them.
+//   * The forward keeps the reference's rounding order exactly when each node's in-edges are in
+//     ascending source order (complete i-major graphs, our k-NN builder):
 //     m = fl(fl(gamma*x) + beta), acc = fl(acc + m) in source order, out = fl(acc / deg).
-//     Non-neighbours are skipped (wave-uniform edge mask).  No FMA contraction.
-//   * Backward: grad_x via the transposed tiles, d gamma / d beta as per-edge
-//     P-length dot products (Gram of grad_out and x planes) reduced with wave shuffles;
-//     no atomics, every output element written by one lane -> deterministic.
+//     Non-neighbours are skipped, never multiplied by zero.  Built with -ffp-contract=off.
+//   * Backward: grad_x via the transposed tiles, d gamma / d beta as per-edge P-length dot
+//     products (Gram of grad_out and x planes) reduced with wave shuffles; no atomics, every
+//     output element written by one lane -> deterministic.
 //   * Everything is HBM-bound (about N/4 flop per byte), so no MFMA here.
 
 #include <hip/hip_runtime.h>
@@ -33,26 +39,26 @@ namespace mrp {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBlock = 256;        // threads per workgroup (4 waves)
+constexpr int kBlock = 256;  // threads per workgroup (4 waves)
 constexpr int kMaxChanPerBlock = 16;
 
 struct AggArgs {
-  const float* x;   // source node features (fwd: x, bwd: x)
-  int64_t xs;       // node stride (elements)
-  const float* g;   // bwd: grad_out
+  const float* x;  // source node features (fwd: x, bwd: x)
+  int64_t xs;      // node stride (elements)
+  const float* g;  // bwd: grad_out
   int64_t gs;
   const float* gb;  // (E, C, 2) interleaved gamma/beta
   const int32_t* indptr;
   const int32_t* src;
   const int32_t* eid;
   const int32_t* goff;
-  float* out;       // fwd: out, bwd: grad_x
+  float* out;  // fwd: out, bwd: grad_x
   int64_t os;
-  float* dgb;       // bwd: grad of gb (E, C, 2)
+  float* dgb;  // bwd: grad of gb (E, C, 2)
   int32_t C, P, PV, mode;
-  int32_t lpc;      // lanes per channel plane (power of two <= 64)
-  int32_t cpb;      // channels per workgroup
-  int32_t ncb;      // channel blocks per graph
+  int32_t lpc;  // lanes per channel plane (power of two <= 64)
+  int32_t cpb;  // channels per workgroup
+  int32_t ncb;  // channel blocks per graph
   int32_t want_dx, want_dgb;
 };
 
@@ -61,26 +67,39 @@ struct Frag {
   float v[VEC];
 };
 
-template <int VEC>
+template <int VEC, bool NTL>
 __device__ __forceinline__ Frag<VEC> load_frag(const float* p) {
   Frag<VEC> f;
   if constexpr (VEC == 4) {
-    const f4 t = *reinterpret_cast<const f4*>(p);
-    f.v[0] = t.x; f.v[1] = t.y; f.v[2] = t.z; f.v[3] = t.w;
+    const f4* q = reinterpret_cast<const f4*>(p);
+    const f4 t = NTL ? __builtin_nontemporal_load(q) : *q;
+    f.v[0] = t.x;
+    f.v[1] = t.y;
+    f.v[2] = t.z;
+    f.v[3] = t.w;
   } else {
-    f.v[0] = *p;
+    f.v[0] = NTL ? __builtin_nontemporal_load(p) : *p;
   }
   return f;
 }
 
-template <int VEC>
+template <int VEC, bool NTL>
 __device__ __forceinline__ void store_frag(float* p, const Frag<VEC>& f) {
   if constexpr (VEC == 4) {
     f4 t;
-    t.x = f.v[0]; t.y = f.v[1]; t.z = f.v[2]; t.w = f.v[3];
-    *reinterpret_cast<f4*>(p) = t;
+    t.x = f.v[0];
+    t.y = f.v[1];
+    t.z = f.v[2];
+    t.w = f.v[3];
+    if (NTL)
+      __builtin_nontemporal_store(t, reinterpret_cast<f4*>(p));
+    else
+      *reinterpret_cast<f4*>(p) = t;
   } else {
-    *p = f.v[0];
+    if (NTL)
+      __builtin_nontemporal_store(f.v[0], p);
+    else
+      *p = f.v[0];
   }
 }
 
@@ -90,20 +109,26 @@ struct Tile {
   static constexpr int SZ = NT * NTP;        // floats per channel tile
 };
 
+// Edge id of u -> v (u != v) in a complete graph of n nodes whose edges start at ebase and are
+// numbered i-major over ordered pairs (dgl/dataloader.py:88-95).
+__device__ __forceinline__ int64_t complete_eid(int64_t ebase, int n, int u, int v) {
+  return ebase + (int64_t)u * (n - 1) + (v < u ? v : v - 1);
+}
+
 // ---------------------------------------------------------------------------
-// Prologue: dense per-channel weight tiles from the CSR-by-destination graph.
+// Prologue, CSR graphs: dense per-channel weight tiles from the CSR-by-destination graph.
 //
 //   FWD  : Ga[cl][v][u] = sum of gamma over edges u->v (1 per edge for COPY),
 //          Gb[cl][v][u] = sum of beta  over edges u->v (0 for COPY),
-//          degf[v]      = in-degree (float).
-//   BWD  : Wt[cl][u][v] = s_v * Ga[cl][v][u]  (transposed, scaled by the reduce
+//          sc[v] = in-degree (float), emask[v] = neighbour bits.
+//   BWD  : Ga[cl][u][v] = s_v * sum of gamma over edges u->v  (transposed, scaled by the reduce
 //          scale s_v = 1/deg v (mean) or 1 (sum)); sc[v] = s_v.
-// Each (channel, v) row is built by one thread walking v's in-edges in CSR order,
-// so there are no LDS races, including for multi-edges.
+// Each (channel, v) row is built by one thread walking v's in-edges in CSR order, so there are
+// no LDS races, including for multi-edges.
 // ---------------------------------------------------------------------------
 template <int NT, bool BWD>
-__device__ __forceinline__ void build_tiles(const AggArgs& a, int node0, int n, int c0,
-                                            float* Ga, float* Gb, float* sc, unsigned* emask) {
+__device__ __forceinline__ void build_tiles_csr(const AggArgs& a, int node0, int n, int c0, float* Ga,
+                                                float* Gb, float* sc, unsigned* emask) {
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
   const int tid = threadIdx.x;
@@ -151,13 +176,86 @@ __device__ __forceinline__ void build_tiles(const AggArgs& a, int node0, int n, 
       if (!BWD) emask[v] = 0u;
     }
   }
-  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Prologue, COMPLETE graphs of exactly NT nodes: the gamma/beta of LDS slot (cl, v, u) is one
+// load at an arithmetic edge id, so the whole tile set is one round of independent loads.
+// Split in two so the caller can issue its first feature loads between them:
+//   complete_fetch : per-thread registers <- gamma/beta of the slots this thread owns
+//   complete_store : registers -> LDS (FWD layout [v][u] gamma and beta; BWD layout [u][v]
+//                    scaled gamma)
+// ---------------------------------------------------------------------------
+template <int NT>
+struct CompleteSlots {
+  static constexpr int kSlots = NT * NT;
+  static constexpr int kPer = (kMaxChanPerBlock * kSlots + kBlock - 1) / kBlock;  // max slots per thread
+};
+
+template <int NT>
+__device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, int c0, int base, float2* reg) {
+  constexpr int S = CompleteSlots<NT>::kSlots;
+  const int tot = a.cpb * S;
+#pragma unroll
+  for (int r = 0; r < CompleteSlots<NT>::kPer; ++r) {
+    const int t = base + threadIdx.x + r * blockDim.x;
+    float2 val = make_float2(0.f, 0.f);
+    if (t < tot) {
+      const int cl = t % a.cpb;  // channel fastest -> neighbouring lanes read neighbouring pairs
+      const int slot = t / a.cpb;
+      const int v = slot / NT, u = slot - v * NT;
+      const int c = c0 + cl;
+      if (u != v && c < a.C) {
+        if (a.mode == MRP_AGG_COPY_MEAN) {
+          val = make_float2(1.f, 0.f);
+        } else {
+          val = *reinterpret_cast<const float2*>(a.gb + (complete_eid(ebase, NT, u, v) * a.C + c) * 2);
+        }
+      }
+    }
+    reg[r] = val;
+  }
+}
+
+template <int NT, bool BWD>
+__device__ __forceinline__ void complete_store(const AggArgs& a, int base, const float2* reg, float* Ga, float* Gb) {
+  constexpr int S = CompleteSlots<NT>::kSlots;
+  constexpr int SZ = Tile<NT>::SZ;
+  constexpr int NTP = Tile<NT>::NTP;
+  const int tot = a.cpb * S;
+  const float s = (BWD && a.mode != MRP_AGG_FILM_SUM && NT > 1) ? 1.f / (float)(NT - 1) : 1.f;
+#pragma unroll
+  for (int r = 0; r < CompleteSlots<NT>::kPer; ++r) {
+    const int t = base + threadIdx.x + r * blockDim.x;
+    if (t < tot) {
+      const int cl = t % a.cpb;
+      const int slot = t / a.cpb;
+      const int v = slot / NT, u = slot - v * NT;
+      if (BWD) {
+        Ga[cl * SZ + u * NTP + v] = s * reg[r].x;
+      } else {
+        Ga[cl * SZ + v * NTP + u] = reg[r].x;
+        Gb[cl * SZ + v * NTP + u] = reg[r].y;
+      }
+    }
+  }
+}
+
+// Remaining slot chunks (only when a small workgroup owns more than kPer slots per thread).
+template <int NT, bool BWD>
+__device__ __forceinline__ void complete_rest(const AggArgs& a, int64_t ebase, int c0, float* Ga, float* Gb) {
+  const int chunk = CompleteSlots<NT>::kPer * blockDim.x;
+  for (int base = chunk; base < a.cpb * CompleteSlots<NT>::kSlots; base += chunk) {
+    float2 reg[CompleteSlots<NT>::kPer];
+    complete_fetch<NT>(a, ebase, c0, base, reg);
+    complete_store<NT, BWD>(a, base, reg, Ga, Gb);
+  }
 }
 
 // ---------------------------------------------------------------------------
 // Forward.  out[v] = reduce_{e=(u->v)} (gamma_e * x_u + beta_e), zero if deg v == 0.
 // ---------------------------------------------------------------------------
-template <int NT, int VEC>
+template <int NT, int VEC, bool COMPLETE>
 __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
@@ -170,38 +268,58 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
 
   const int b = blockIdx.x / a.ncb;
   const int cb = blockIdx.x - b * a.ncb;
-  const int node0 = a.goff[b];
-  const int n = min(a.goff[b + 1] - node0, NT);
+  const int node0 = COMPLETE ? b * NT : a.goff[b];
+  const int n = COMPLETE ? NT : min(a.goff[b + 1] - node0, NT);
   if (n <= 0) return;  // whole workgroup: empty graph
   const int c0 = cb * a.cpb;
-
-  build_tiles<NT, false>(a, node0, n, c0, Ga, Gb, degf, emask);
 
   const int grp = threadIdx.x / a.lpc;
   const int li = threadIdx.x - grp * a.lpc;
   const int c = c0 + grp;
-  if (grp >= a.cpb || c >= a.C) return;
-
+  const bool active = grp < a.cpb && c < a.C;
   const float* xb = a.x + (int64_t)node0 * a.xs + (int64_t)c * a.P;
   float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
-  const float* A = Ga + grp * SZ;
-  const float* Bt = Gb + grp * SZ;
+
+  // prologue part 1 (COMPLETE): gamma/beta into registers
+  float2 reg[CompleteSlots<NT>::kPer];
+  const int64_t ebase = (int64_t)b * NT * (NT - 1);
+  if (COMPLETE) complete_fetch<NT>(a, ebase, c0, 0, reg);
+  // first slice of the sweep, issued before the weight tiles are needed
+  int j = li;
+  Frag<VEC> xv[NT];
+  if (active && j < a.PV) {
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      const int uu = u < n ? u : n - 1;  // clamp (ragged batch); never used for output
+      xv[u] = load_frag<VEC, true>(xb + (int64_t)uu * a.xs + (int64_t)j * VEC);
+    }
+  }
+  // prologue part 2: tiles into LDS
+  if (COMPLETE) {
+    complete_store<NT, false>(a, 0, reg, Ga, Gb);
+    complete_rest<NT, false>(a, ebase, c0, Ga, Gb);
+  } else
+    build_tiles_csr<NT, false>(a, node0, n, c0, Ga, Gb, degf, emask);
+  __syncthreads();
+  if (!active) return;
+
   const bool film = a.mode != MRP_AGG_COPY_MEAN;
   const bool mean = a.mode != MRP_AGG_FILM_SUM;
 
-  for (int j = li; j < a.PV; j += a.lpc) {
+  while (j < a.PV) {
     const int64_t off = (int64_t)j * VEC;
-    Frag<VEC> xv[NT];
-#pragma unroll
-    for (int u = 0; u < NT; ++u) {
-      const int uu = u < n ? u : n - 1;  // clamp (ragged batch); weight is 0 there
-      xv[u] = load_frag<VEC>(xb + (int64_t)uu * a.xs + off);
-    }
+    // Re-read the tiles from LDS every slice: laundering the tile offset stops the compiler from
+    // hoisting all N*N weights into registers (which would cost occupancy or spill).
+    int tile = grp * SZ;
+    asm volatile("" : "+v"(tile));
+    const float* A = Ga + tile;
+    const float* Bt = Gb + tile;
 #pragma unroll
     for (int v = 0; v < NT; ++v) {
-      if (v >= n) break;
-      // Edge mask of v: channel independent, so wave-uniform -> scalar branches.
-      const unsigned em = __builtin_amdgcn_readfirstlane(emask[v]);
+      if (!COMPLETE && v >= n) break;
+      // neighbour mask of v: compile-time for COMPLETE, else channel-independent -> wave-uniform
+      const unsigned em =
+          COMPLETE ? (((1u << NT) - 1u) & ~(1u << v)) : __builtin_amdgcn_readfirstlane(emask[v]);
       Frag<VEC> acc;
 #pragma unroll
       for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
@@ -218,28 +336,34 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
           const float gbv = wb[q];
 #pragma unroll
           for (int k = 0; k < VEC; ++k) {
-            float m;
-            if (film) m = __fadd_rn(__fmul_rn(ga, xv[u].v[k]), gbv);
-            else m = __fmul_rn(ga, xv[u].v[k]);
+            const float m = film ? __fadd_rn(__fmul_rn(ga, xv[u].v[k]), gbv) : __fmul_rn(ga, xv[u].v[k]);
             acc.v[k] = __fadd_rn(acc.v[k], m);
           }
         }
       }
-      const float d = degf[v];
+      const float d = COMPLETE ? (float)(NT - 1) : degf[v];
       if (mean && d > 0.f) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc.v[k] = acc.v[k] / d;
       }
-      store_frag<VEC>(ob + (int64_t)v * a.os + off, acc);
+      store_frag<VEC, true>(ob + (int64_t)v * a.os + off, acc);
+    }
+    j += a.lpc;
+    if (j < a.PV) {
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        const int uu = u < n ? u : n - 1;
+        xv[u] = load_frag<VEC, true>(xb + (int64_t)uu * a.xs + (int64_t)j * VEC);
+      }
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// Backward, grad_x only (used for NT > 8, where the fused kernel's Gram
-// accumulators would not fit in registers):  grad_x[u] = sum_v Wt[u][v] * G[v].
+// Backward, grad_x only (used for NT > 8, where the fused kernel's Gram accumulators would not
+// fit in registers):  grad_x[u] = sum_v Wt[u][v] * G[v].
 // ---------------------------------------------------------------------------
-template <int NT, int VEC>
+template <int NT, int VEC, bool COMPLETE>
 __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
@@ -250,12 +374,20 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
 
   const int b = blockIdx.x / a.ncb;
   const int cb = blockIdx.x - b * a.ncb;
-  const int node0 = a.goff[b];
-  const int n = min(a.goff[b + 1] - node0, NT);
+  const int node0 = COMPLETE ? b * NT : a.goff[b];
+  const int n = COMPLETE ? NT : min(a.goff[b + 1] - node0, NT);
   if (n <= 0) return;
   const int c0 = cb * a.cpb;
 
-  build_tiles<NT, true>(a, node0, n, c0, Wt, nullptr, sc, nullptr);
+  if (COMPLETE) {
+    float2 reg[CompleteSlots<NT>::kPer];
+    complete_fetch<NT>(a, (int64_t)b * NT * (NT - 1), c0, 0, reg);
+    complete_store<NT, true>(a, 0, reg, Wt, nullptr);
+    complete_rest<NT, true>(a, (int64_t)b * NT * (NT - 1), c0, Wt, nullptr);
+  } else {
+    build_tiles_csr<NT, true>(a, node0, n, c0, Wt, nullptr, sc, nullptr);
+  }
+  __syncthreads();
 
   const int grp = threadIdx.x / a.lpc;
   const int li = threadIdx.x - grp * a.lpc;
@@ -264,19 +396,21 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
 
   const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c * a.P;
   float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
-  const float* W = Wt + grp * SZ;
 
   for (int j = li; j < a.PV; j += a.lpc) {
     const int64_t off = (int64_t)j * VEC;
+    int tile = grp * SZ;  // laundered: keep the weights in LDS, not hoisted into registers
+    asm volatile("" : "+v"(tile));
+    const float* W = Wt + tile;
     Frag<VEC> gv[NT];
 #pragma unroll
     for (int v = 0; v < NT; ++v) {
       const int vv = v < n ? v : n - 1;
-      gv[v] = load_frag<VEC>(gbase + (int64_t)vv * a.gs + off);
+      gv[v] = load_frag<VEC, true>(gbase + (int64_t)vv * a.gs + off);
     }
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
-      if (u >= n) break;
+      if (!COMPLETE && u >= n) break;
       Frag<VEC> acc;
 #pragma unroll
       for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
@@ -287,11 +421,12 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
         for (int q = 0; q < 4; ++q) {
           const int v = v4 + q;
           if (v >= NT) break;
+          if (COMPLETE && v == u) continue;
 #pragma unroll
           for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(w[q], gv[v].v[k], acc.v[k]);
         }
       }
-      store_frag<VEC>(ob + (int64_t)u * a.os + off, acc);
+      store_frag<VEC, true>(ob + (int64_t)u * a.os + off, acc);
     }
   }
 }
@@ -303,31 +438,40 @@ __device__ __forceinline__ float group_sum(float x, int lpc) {
 }
 
 // ---------------------------------------------------------------------------
-// Backward, fused: one sweep reads G and x once, writes grad_x (if VB == NT and
-// want_dx) and accumulates the per-channel Gram D[v][u] = sum_p G_v * x_u and
-// S[v] = sum_p G_v for a block of VB destination rows; then writes
+// Backward, fused: one sweep reads G and x once, writes grad_x (if VB == NT and want_dx) and
+// accumulates the per-channel Gram D[v][u] = sum_p G_v * x_u and S[v] = sum_p G_v for a block of
+// VB destination rows; then writes
 //   grad_gb[e, c] = (s_v * D[v][u], s_v * S[v])    for every edge e = (u -> v).
-// For NT > 8 the kernel runs with VB = 4 and loops over destination blocks.
+// For NT > 8 the kernel runs with VB = 4 and loops over destination blocks (x re-read from L2).
 // ---------------------------------------------------------------------------
-template <int NT, int VB, int VEC>
+template <int NT, int VB, int VEC, bool COMPLETE>
 __global__ void __launch_bounds__(kBlock) film_bwd_fused(AggArgs a) {
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
+  constexpr bool kOnePass = VB == NT;
   extern __shared__ float4 smem_f4[];
   float* smem = reinterpret_cast<float*>(smem_f4);
-  float* Wt = smem;                     // [cpb][NT][NTP]   scaled, transposed
-  float* Dl = Wt + a.cpb * SZ;          // [cpb][NT][NTP]   Gram (unscaled)
-  float* Sl = Dl + a.cpb * SZ;          // [cpb][NTP]       sum_p G_v
-  float* sc = Sl + a.cpb * NTP;         // [NTP]            s_v
+  float* Wt = smem;              // [cpb][NT][NTP]   scaled, transposed
+  float* Dl = Wt + a.cpb * SZ;   // [cpb][NT][NTP]   Gram (unscaled)
+  float* Sl = Dl + a.cpb * SZ;   // [cpb][NTP]       sum_p G_v
+  float* sc = Sl + a.cpb * NTP;  // [NTP]            s_v
 
   const int b = blockIdx.x / a.ncb;
   const int cb = blockIdx.x - b * a.ncb;
-  const int node0 = a.goff[b];
-  const int n = min(a.goff[b + 1] - node0, NT);
+  const int node0 = COMPLETE ? b * NT : a.goff[b];
+  const int n = COMPLETE ? NT : min(a.goff[b + 1] - node0, NT);
   if (n <= 0) return;
   const int c0 = cb * a.cpb;
 
-  build_tiles<NT, true>(a, node0, n, c0, Wt, nullptr, sc, nullptr);
+  if (COMPLETE) {
+    float2 reg[CompleteSlots<NT>::kPer];
+    complete_fetch<NT>(a, (int64_t)b * NT * (NT - 1), c0, 0, reg);
+    complete_store<NT, true>(a, 0, reg, Wt, nullptr);
+    complete_rest<NT, true>(a, (int64_t)b * NT * (NT - 1), c0, Wt, nullptr);
+  } else {
+    build_tiles_csr<NT, true>(a, node0, n, c0, Wt, nullptr, sc, nullptr);
+  }
+  __syncthreads();
 
   const int grp = threadIdx.x / a.lpc;
   const int li = threadIdx.x - grp * a.lpc;
@@ -337,8 +481,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_fused(AggArgs a) {
   const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c * a.P;
   const float* xbase = a.x + (int64_t)node0 * a.xs + (int64_t)c * a.P;
   float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
-  const float* W = Wt + grp * SZ;
-  const bool do_dx = (VB == NT) && a.want_dx;
+  const bool do_dx = kOnePass && a.want_dx;
 
 #pragma unroll 1
   for (int vb = 0; vb < NT; vb += VB) {
@@ -353,25 +496,28 @@ __global__ void __launch_bounds__(kBlock) film_bwd_fused(AggArgs a) {
     if (active) {
       for (int j = li; j < a.PV; j += a.lpc) {
         const int64_t off = (int64_t)j * VEC;
+        int tile = grp * SZ;  // laundered: keep the weights in LDS, not hoisted into registers
+        asm volatile("" : "+v"(tile));
+        const float* W = Wt + tile;
         Frag<VEC> gv[VB];
         Frag<VEC> xv[NT];
 #pragma unroll
         for (int i = 0; i < VB; ++i) {
           const int v = vb + i;
           const int vv = v < n ? v : n - 1;
-          gv[i] = load_frag<VEC>(gbase + (int64_t)vv * a.gs + off);
+          gv[i] = load_frag<VEC, kOnePass>(gbase + (int64_t)vv * a.gs + off);
         }
         if (a.want_dgb) {
 #pragma unroll
           for (int u = 0; u < NT; ++u) {
             const int uu = u < n ? u : n - 1;
-            xv[u] = load_frag<VEC>(xbase + (int64_t)uu * a.xs + off);
+            xv[u] = load_frag<VEC, kOnePass>(xbase + (int64_t)uu * a.xs + off);
           }
         }
         if (do_dx) {
 #pragma unroll
           for (int u = 0; u < NT; ++u) {
-            if (u >= n) break;
+            if (!COMPLETE && u >= n) break;
             Frag<VEC> acc;
 #pragma unroll
             for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
@@ -382,11 +528,12 @@ __global__ void __launch_bounds__(kBlock) film_bwd_fused(AggArgs a) {
               for (int q = 0; q < 4; ++q) {
                 const int v = v4 + q;
                 if (v >= NT) break;
+                if (COMPLETE && v == u) continue;
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(w[q], gv[v].v[k], acc.v[k]);
               }
             }
-            store_frag<VEC>(ob + (int64_t)u * a.os + off, acc);
+            store_frag<VEC, true>(ob + (int64_t)u * a.os + off, acc);
           }
         }
         if (a.want_dgb) {
@@ -396,6 +543,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_fused(AggArgs a) {
             for (int k = 0; k < VEC; ++k) S[i] += gv[i].v[k];
 #pragma unroll
             for (int u = 0; u < NT; ++u) {
+              if (COMPLETE && kOnePass && u == i) continue;  // not an edge
 #pragma unroll
               for (int k = 0; k < VEC; ++k) D[i][u] = fmaf(gv[i].v[k], xv[u].v[k], D[i][u]);
             }
@@ -404,13 +552,16 @@ __global__ void __launch_bounds__(kBlock) film_bwd_fused(AggArgs a) {
       }
     }
     if (a.want_dgb) {
-      // Reduce across the lanes of each channel group (all lanes of the wave take
-      // part in the shuffles; inactive groups contribute zeros to their own group).
+      // Reduce across the lanes of each channel group (all lanes of the wave take part in the
+      // shuffles; inactive groups contribute zeros to their own group).
 #pragma unroll
       for (int i = 0; i < VB; ++i) {
         S[i] = group_sum(S[i], a.lpc);
 #pragma unroll
-        for (int u = 0; u < NT; ++u) D[i][u] = group_sum(D[i][u], a.lpc);
+        for (int u = 0; u < NT; ++u) {
+          if (COMPLETE && kOnePass && u == i) continue;
+          D[i][u] = group_sum(D[i][u], a.lpc);
+        }
       }
       if (active && li == 0) {
 #pragma unroll
@@ -427,9 +578,24 @@ __global__ void __launch_bounds__(kBlock) film_bwd_fused(AggArgs a) {
   }
   if (!a.want_dgb) return;
   __syncthreads();
-  // Per-edge outputs.  Thread -> (channel fastest, destination v); the in-edges
-  // of v are walked in CSR order.  Every edge of the graph has exactly one
-  // destination here, so each grad_gb element is written once.
+  if (COMPLETE) {
+    // Per-edge outputs: thread -> (channel fastest, slot (v, u)); arithmetic edge ids.
+    const float s = (a.mode != MRP_AGG_FILM_SUM && NT > 1) ? 1.f / (float)(NT - 1) : 1.f;
+    const int64_t ebase = (int64_t)b * NT * (NT - 1);
+    for (int t = threadIdx.x; t < a.cpb * NT * NT; t += blockDim.x) {
+      const int cl = t % a.cpb;
+      const int slot = t / a.cpb;
+      const int v = slot / NT, u = slot - v * NT;
+      const int cc = c0 + cl;
+      if (u == v || cc >= a.C) continue;
+      const float2 r = make_float2(s * Dl[cl * SZ + v * NTP + u], s * Sl[cl * NTP + v]);
+      *reinterpret_cast<float2*>(a.dgb + (complete_eid(ebase, NT, u, v) * a.C + cc) * 2) = r;
+    }
+    return;
+  }
+  // CSR: thread -> (channel fastest, destination v); the in-edges of v are walked in CSR order.
+  // Every edge of the graph has exactly one destination here, so each grad_gb element is
+  // written once.
   for (int t = threadIdx.x; t < a.cpb * NT; t += blockDim.x) {
     const int cl = t % a.cpb;
     const int v = t / a.cpb;
@@ -446,9 +612,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_fused(AggArgs a) {
         dgam = s * Dl[cl * SZ + v * NTP + u];
         dbet = dbeta;
       }
-      float* q = a.dgb + ((int64_t)a.eid[k] * a.C + cc) * 2;
-      q[0] = dgam;
-      q[1] = dbet;
+      *reinterpret_cast<float2*>(a.dgb + ((int64_t)a.eid[k] * a.C + cc) * 2) = make_float2(dgam, dbet);
     }
   }
 }
@@ -496,91 +660,97 @@ size_t lds_dx(int cpb) {
 }
 template <int NT>
 size_t lds_bwd(int cpb) {
-  return (size_t)(2 * cpb * mrp::Tile<NT>::SZ + cpb * mrp::Tile<NT>::NTP + mrp::Tile<NT>::NTP) *
-         sizeof(float);
+  return (size_t)(2 * cpb * mrp::Tile<NT>::SZ + cpb * mrp::Tile<NT>::NTP + mrp::Tile<NT>::NTP) * sizeof(float);
 }
 
-template <int NT>
+#define MRP_LAUNCH(KERNEL, LDS) hipLaunchKernelGGL((KERNEL), dim3((unsigned)g.grid), dim3(g.threads), (LDS), st, a)
+
+template <int NT, bool COMPLETE>
 hipError_t launch_fwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
   const size_t lds = lds_fwd<NT>(g.cpb);
   if (g.vec == 4)
-    hipLaunchKernelGGL((mrp::film_fwd<NT, 4>), dim3((unsigned)g.grid), dim3(g.threads), lds, st, a);
+    MRP_LAUNCH((mrp::film_fwd<NT, 4, COMPLETE>), lds);
   else
-    hipLaunchKernelGGL((mrp::film_fwd<NT, 1>), dim3((unsigned)g.grid), dim3(g.threads), lds, st, a);
+    MRP_LAUNCH((mrp::film_fwd<NT, 1, COMPLETE>), lds);
   return hipGetLastError();
 }
 
-template <int NT>
-hipError_t launch_bwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
+template <int NT, bool COMPLETE>
+hipError_t launch_bwd_nt(const AggArgs& a_in, const Geometry& g, hipStream_t st) {
   if constexpr (NT <= 8) {
+    const AggArgs& a = a_in;
     const size_t lds = lds_bwd<NT>(g.cpb);
     if (g.vec == 4)
-      hipLaunchKernelGGL((mrp::film_bwd_fused<NT, NT, 4>), dim3((unsigned)g.grid), dim3(g.threads), lds,
-                         st, a);
+      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 4, COMPLETE>), lds);
     else
-      hipLaunchKernelGGL((mrp::film_bwd_fused<NT, NT, 1>), dim3((unsigned)g.grid), dim3(g.threads), lds,
-                         st, a);
+      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 1, COMPLETE>), lds);
     return hipGetLastError();
   } else {
-    if (a.want_dx) {
+    if (a_in.want_dx) {
+      const AggArgs& a = a_in;
       const size_t lds = lds_dx<NT>(g.cpb);
       if (g.vec == 4)
-        hipLaunchKernelGGL((mrp::film_bwd_dx<NT, 4>), dim3((unsigned)g.grid), dim3(g.threads), lds, st, a);
+        MRP_LAUNCH((mrp::film_bwd_dx<NT, 4, COMPLETE>), lds);
       else
-        hipLaunchKernelGGL((mrp::film_bwd_dx<NT, 1>), dim3((unsigned)g.grid), dim3(g.threads), lds, st, a);
+        MRP_LAUNCH((mrp::film_bwd_dx<NT, 1, COMPLETE>), lds);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
-    if (a.want_dgb) {
-      AggArgs b = a;
-      b.want_dx = 0;
+    if (a_in.want_dgb) {
+      AggArgs a = a_in;
+      a.want_dx = 0;
       const size_t lds = lds_bwd<NT>(g.cpb);
       if (g.vec == 4)
-        hipLaunchKernelGGL((mrp::film_bwd_fused<NT, 4, 4>), dim3((unsigned)g.grid), dim3(g.threads), lds,
-                           st, b);
+        MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 4, COMPLETE>), lds);
       else
-        hipLaunchKernelGGL((mrp::film_bwd_fused<NT, 4, 1>), dim3((unsigned)g.grid), dim3(g.threads), lds,
-                           st, b);
+        MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 1, COMPLETE>), lds);
       return hipGetLastError();
     }
     return hipSuccess;
   }
 }
 
-#define MRP_DISPATCH_NT(NTV, FN, ...) \
-  switch (NTV) {                      \
-    case 1: return FN<1>(__VA_ARGS__);   \
-    case 2: return FN<2>(__VA_ARGS__);   \
-    case 3: return FN<3>(__VA_ARGS__);   \
-    case 4: return FN<4>(__VA_ARGS__);   \
-    case 5: return FN<5>(__VA_ARGS__);   \
-    case 6: return FN<6>(__VA_ARGS__);   \
-    case 7: return FN<7>(__VA_ARGS__);   \
-    case 8: return FN<8>(__VA_ARGS__);   \
-    case 9: return FN<9>(__VA_ARGS__);   \
-    case 10: return FN<10>(__VA_ARGS__); \
-    case 11: return FN<11>(__VA_ARGS__); \
-    case 12: return FN<12>(__VA_ARGS__); \
-    case 13: return FN<13>(__VA_ARGS__); \
-    case 14: return FN<14>(__VA_ARGS__); \
-    case 15: return FN<15>(__VA_ARGS__); \
-    case 16: return FN<16>(__VA_ARGS__); \
-    default: return hipErrorInvalidValue; \
+#define MRP_DISPATCH_NT(NTV, COMPLETE, FN, ...)                                        \
+  switch (NTV) {                                                                       \
+    case 1: return COMPLETE ? FN<1, true>(__VA_ARGS__) : FN<1, false>(__VA_ARGS__);    \
+    case 2: return COMPLETE ? FN<2, true>(__VA_ARGS__) : FN<2, false>(__VA_ARGS__);    \
+    case 3: return COMPLETE ? FN<3, true>(__VA_ARGS__) : FN<3, false>(__VA_ARGS__);    \
+    case 4: return COMPLETE ? FN<4, true>(__VA_ARGS__) : FN<4, false>(__VA_ARGS__);    \
+    case 5: return COMPLETE ? FN<5, true>(__VA_ARGS__) : FN<5, false>(__VA_ARGS__);    \
+    case 6: return COMPLETE ? FN<6, true>(__VA_ARGS__) : FN<6, false>(__VA_ARGS__);    \
+    case 7: return COMPLETE ? FN<7, true>(__VA_ARGS__) : FN<7, false>(__VA_ARGS__);    \
+    case 8: return COMPLETE ? FN<8, true>(__VA_ARGS__) : FN<8, false>(__VA_ARGS__);    \
+    case 9: return COMPLETE ? FN<9, true>(__VA_ARGS__) : FN<9, false>(__VA_ARGS__);    \
+    case 10: return COMPLETE ? FN<10, true>(__VA_ARGS__) : FN<10, false>(__VA_ARGS__); \
+    case 11: return COMPLETE ? FN<11, true>(__VA_ARGS__) : FN<11, false>(__VA_ARGS__); \
+    case 12: return COMPLETE ? FN<12, true>(__VA_ARGS__) : FN<12, false>(__VA_ARGS__); \
+    case 13: return COMPLETE ? FN<13, true>(__VA_ARGS__) : FN<13, false>(__VA_ARGS__); \
+    case 14: return COMPLETE ? FN<14, true>(__VA_ARGS__) : FN<14, false>(__VA_ARGS__); \
+    case 15: return COMPLETE ? FN<15, true>(__VA_ARGS__) : FN<15, false>(__VA_ARGS__); \
+    case 16: return COMPLETE ? FN<16, true>(__VA_ARGS__) : FN<16, false>(__VA_ARGS__); \
+    default: return hipErrorInvalidValue;                                              \
   }
 
-hipError_t dispatch_fwd(int nt, const AggArgs& a, const Geometry& g, hipStream_t st) {
-  MRP_DISPATCH_NT(nt, launch_fwd_nt, a, g, st)
+hipError_t dispatch_fwd(int nt, bool complete, const AggArgs& a, const Geometry& g, hipStream_t st) {
+  MRP_DISPATCH_NT(nt, complete, launch_fwd_nt, a, g, st)
 }
-hipError_t dispatch_bwd(int nt, const AggArgs& a, const Geometry& g, hipStream_t st) {
-  MRP_DISPATCH_NT(nt, launch_bwd_nt, a, g, st)
+hipError_t dispatch_bwd(int nt, bool complete, const AggArgs& a, const Geometry& g, hipStream_t st) {
+  MRP_DISPATCH_NT(nt, complete, launch_bwd_nt, a, g, st)
 }
 
-bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* eid,
-                    const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes,
-                    int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode) {
+bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* eid, const int32_t* graph_off,
+                    int32_t num_graphs, int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges,
+                    int32_t C, int32_t P, int32_t mode) {
   if (num_graphs < 0 || num_nodes < 0 || num_edges < 0 || C < 0 || P < 0) return false;
   if (max_nodes < 0 || max_nodes > MRP_MAX_NODES) return false;
   if (mode < MRP_AGG_FILM_MEAN || mode > MRP_AGG_COPY_MEAN) return false;
+  if (graph_kind == MRP_GRAPH_COMPLETE) {
+    // every graph: exactly max_nodes nodes, all ordered pairs, numbered graph by graph
+    if ((int64_t)num_graphs * max_nodes != num_nodes) return false;
+    if ((int64_t)num_graphs * max_nodes * (max_nodes > 0 ? max_nodes - 1 : 0) != num_edges) return false;
+    return true;
+  }
+  if (graph_kind != MRP_GRAPH_CSR) return false;
   if (num_graphs > 0 && graph_off == nullptr) return false;
   if (num_nodes > 0 && indptr == nullptr) return false;
   if (num_edges > 0 && (src == nullptr || eid == nullptr)) return false;
@@ -592,23 +762,24 @@ bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* ei
 
 extern "C" {
 
-int mrp_abi_version(void) { return 1; }
+int mrp_abi_version(void) { return 2; }
 
 const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
 
 int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr,
                       const int32_t* src, const int32_t* eid, const int32_t* graph_off, int32_t num_graphs,
-                      int32_t max_nodes, int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P,
-                      int32_t mode, float* out, int64_t out_node_stride, void* stream) {
-  if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, num_nodes, num_edges, C, P, mode))
+                      int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C,
+                      int32_t P, int32_t mode, float* out, int64_t out_node_stride, void* stream) {
+  if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind, num_nodes, num_edges, C, P,
+                      mode))
     return hipErrorInvalidValue;
   if (num_graphs == 0 || num_nodes == 0 || max_nodes == 0 || C == 0 || P == 0) return hipSuccess;
   const int64_t plane = (int64_t)C * P;
   if (x == nullptr || out == nullptr || x_node_stride < plane || out_node_stride < plane)
     return hipErrorInvalidValue;
   if (mode != MRP_AGG_COPY_MEAN && num_edges > 0 && gb == nullptr) return hipErrorInvalidValue;
-  const bool vec4 = (P % 4 == 0) && (x_node_stride % 4 == 0) && (out_node_stride % 4 == 0) && aligned16(x) &&
-                    aligned16(out);
+  const bool vec4 =
+      (P % 4 == 0) && (x_node_stride % 4 == 0) && (out_node_stride % 4 == 0) && aligned16(x) && aligned16(out);
   Geometry g = make_geometry(C, P, vec4);
   g.grid = (int64_t)num_graphs * g.ncb;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
@@ -629,15 +800,16 @@ int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, co
   a.lpc = g.lpc;
   a.cpb = g.cpb;
   a.ncb = g.ncb;
-  return dispatch_fwd(max_nodes, a, g, static_cast<hipStream_t>(stream));
+  return dispatch_fwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, static_cast<hipStream_t>(stream));
 }
 
 int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float* x, int64_t x_node_stride,
                       const float* gb, const int32_t* indptr, const int32_t* src, const int32_t* eid,
-                      const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes, int32_t num_nodes,
-                      int32_t num_edges, int32_t C, int32_t P, int32_t mode, float* grad_x,
+                      const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
+                      int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode, float* grad_x,
                       int64_t gx_node_stride, float* grad_gb, void* stream) {
-  if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, num_nodes, num_edges, C, P, mode))
+  if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind, num_nodes, num_edges, C, P,
+                      mode))
     return hipErrorInvalidValue;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool copy = mode == MRP_AGG_COPY_MEAN;
@@ -683,7 +855,7 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   a.ncb = g.ncb;
   a.want_dx = want_dx ? 1 : 0;
   a.want_dgb = want_dgb ? 1 : 0;
-  return dispatch_bwd(max_nodes, a, g, st);
+  return dispatch_bwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, st);
 }
 
 }  // extern "C"

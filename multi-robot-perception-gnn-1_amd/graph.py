@@ -24,7 +24,7 @@ from typing import Dict, Iterable, List, NamedTuple, Optional, Sequence
 import numpy as np
 import torch
 
-from ._lib import MAX_NODES
+from ._lib import GRAPH_COMPLETE, GRAPH_CSR, MAX_NODES
 from .pose import relative_pose_batch
 
 
@@ -39,6 +39,7 @@ class GraphCSR(NamedTuple):
     max_nodes: int
     num_nodes: int
     num_edges: int
+    graph_kind: int  # GRAPH_COMPLETE (the reference topology, arithmetic edge ids) or GRAPH_CSR
 
 
 class _FeatureDict(dict):
@@ -149,6 +150,7 @@ class RobotGraph:
             g.edata[k] = v.to(device, non_blocking=non_blocking)
         g._csr_cache = self._csr_cache  # structure is shared, so is its device CSR
         g._host_csr = self._host_csr
+        g._complete = getattr(self, "_complete", None)
         return g
 
     def cuda(self, device=None) -> "RobotGraph":
@@ -161,16 +163,25 @@ class RobotGraph:
             self._host_csr = build_csr(self._src.numpy(), self._dst.numpy(), self._num_nodes, self._bnn)
         return self._host_csr
 
-    def csr(self, device) -> GraphCSR:
+    def is_complete(self) -> bool:
+        """True when every graph of the batch is the reference's complete graph over the same
+        number of robots with edges in ``complete_edges`` order (``dgl/dataloader.py:88-95``);
+        the kernels then compute edge ids arithmetically instead of walking the CSR."""
+        if getattr(self, "_complete", None) is None:
+            self._complete = is_complete_batch(self._src.numpy(), self._dst.numpy(), self._bnn)
+        return self._complete
+
+    def csr(self, device, allow_complete: bool = True) -> GraphCSR:
         device = torch.device(device)
-        key = str(device)
+        kind = GRAPH_COMPLETE if (allow_complete and self.is_complete()) else GRAPH_CSR
+        key = (str(device), kind)
         hit = self._csr_cache.get(key)
         if hit is not None:
             return hit
         indptr, src, eid, goff, max_nodes = self.host_csr()
         to = lambda a: torch.from_numpy(a).to(device)  # noqa: E731
         csr = GraphCSR(to(indptr), to(src), to(eid), to(goff), len(self._bnn), max_nodes,
-                       self._num_nodes, self.num_edges())
+                       self._num_nodes, self.num_edges(), kind)
         self._csr_cache[key] = csr
         return csr
 
@@ -206,6 +217,25 @@ def build_csr(src: np.ndarray, dst: np.ndarray, num_nodes: int, batch_num_nodes:
     np.cumsum(np.bincount(dst, minlength=num_nodes), out=indptr[1:])
     return (indptr.astype(np.int32), src[order].astype(np.int32), order.astype(np.int32),
             goff.astype(np.int32), max_nodes)
+
+
+def is_complete_batch(src: np.ndarray, dst: np.ndarray, batch_num_nodes: Sequence[int]) -> bool:
+    """Every graph has the same n nodes and exactly the edges of ``complete_edges(n)``, in that
+    order, offset graph by graph (what ``dgl.batch`` of the reference's frames produces)."""
+    if not len(batch_num_nodes):
+        return False
+    n = int(batch_num_nodes[0])
+    B = len(batch_num_nodes)
+    if n < 1 or any(int(v) != n for v in batch_num_nodes) or n > MAX_NODES:
+        return False
+    if len(src) != B * n * (n - 1):
+        return False
+    if n == 1:
+        return True
+    cs, cd = (np.asarray(t, dtype=np.int64) for t in complete_edges(n))
+    off = (np.arange(B, dtype=np.int64) * n)[:, None]
+    return bool(np.array_equal(np.asarray(src).reshape(B, -1), cs[None] + off)
+                and np.array_equal(np.asarray(dst).reshape(B, -1), cd[None] + off))
 
 
 # --------------------------------------------------------------------- constructors

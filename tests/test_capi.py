@@ -50,11 +50,11 @@ def test_abi_version_and_errors():
 
 
 def _fwd(lib, **kw):
-    a = dict(x=None, xs=0, gb=None, indptr=None, src=None, eid=None, goff=None, B=0, maxn=0, Nt=0, E=0,
+    a = dict(x=None, xs=0, gb=None, indptr=None, src=None, eid=None, goff=None, B=0, maxn=0, kind=0, Nt=0, E=0,
              C=0, P=0, mode=0, out=None, os=0, stream=None)
     a.update(kw)
     return lib.mrp_film_mean_fwd(a["x"], a["xs"], a["gb"], a["indptr"], a["src"], a["eid"], a["goff"], a["B"],
-                                 a["maxn"], a["Nt"], a["E"], a["C"], a["P"], a["mode"], a["out"], a["os"],
+                                 a["maxn"], a["kind"], a["Nt"], a["E"], a["C"], a["P"], a["mode"], a["out"], a["os"],
                                  a["stream"])
 
 
@@ -70,8 +70,13 @@ def test_argument_validation_without_launch():
     # stride smaller than a node's C*P block
     assert _fwd(lib, B=1, maxn=2, Nt=2, goff=dummy, indptr=dummy, C=2, P=4, x=dummy, out=dummy, xs=7, os=8,
                 mode=2) == HIP_INVALID_VALUE
+    # unknown graph kind; COMPLETE with inconsistent node / edge counts
+    assert _fwd(lib, kind=2) == HIP_INVALID_VALUE
+    assert _fwd(lib, kind=1, B=2, maxn=4, Nt=8, E=23) == HIP_INVALID_VALUE
+    assert _fwd(lib, kind=1, B=2, maxn=4, Nt=7, E=24) == HIP_INVALID_VALUE
+    assert _fwd(lib, kind=1, B=2, maxn=4, Nt=8, E=24, C=0, P=16) == 0  # consistent, empty features: no-op
     # bwd: nothing requested -> no-op
-    assert lib.mrp_film_mean_bwd(None, 0, None, 0, None, None, None, None, None, 0, 0, 0, 0, 0, 0, 0, None, 0,
+    assert lib.mrp_film_mean_bwd(None, 0, None, 0, None, None, None, None, None, 0, 0, 0, 0, 0, 0, 0, 0, None, 0,
                                  None, None) == 0
 
 

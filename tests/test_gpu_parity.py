@@ -305,3 +305,25 @@ def test_north_star_size_vs_torch_reference(cuda_device):
         a = m.film_mean(x.detach(), gb0, csr)
         b = m.film_mean(2.0 * x.detach(), gb0, csr)
         assert torch.equal(2.0 * a, b)  # scaling by 2 is exact in fp32
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8, 11, 16])
+@pytest.mark.parametrize("hw", [(8, 8), (3, 5)])
+def test_complete_fast_path_equals_csr_path(cuda_device, n, hw):
+    """The COMPLETE kernels (arithmetic edge ids) and the general CSR kernels agree exactly on
+    the forward and to rounding on the backward."""
+    g, x, gb = random_case(n, 12, hw[0], hw[1], seed=200 + n, bnn=[n] * 3)
+    assert g.is_complete()
+    fast, slow = g.csr(cuda_device), g.csr(cuda_device, allow_complete=False)
+    assert fast.graph_kind == 1 and slow.graph_kind == 0
+    G = torch.randn_like(x).to(cuda_device)
+    res = []
+    for csr in (fast, slow):
+        xd = x.to(cuda_device).requires_grad_(True)
+        gbd = gb.to(cuda_device).requires_grad_(True)
+        out = m.film_mean(xd, gbd, csr)
+        out.backward(G)
+        res.append((out.detach().cpu(), xd.grad.cpu(), gbd.grad.cpu()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert rel_err(res[0][1].numpy(), res[1][1].numpy()) <= 1e-6
+    assert rel_err(res[0][2].numpy(), res[1][2].numpy()) <= 1e-6

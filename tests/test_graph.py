@@ -104,3 +104,17 @@ def test_build_csr_multiedge_and_selfloop():
     indptr, src, eid, goff, mx = build_csr(np.array([0, 0, 2, 1]), np.array([1, 1, 2, 1]), 3, [3])
     assert indptr.tolist() == [0, 0, 3, 4]
     assert eid.tolist() == [0, 1, 3, 2] and src.tolist() == [0, 0, 1, 2]
+
+
+def test_is_complete_detection():
+    rng = np.random.RandomState(0)
+    frames = [m.frame_graph(rng.randn(5, 7)) for _ in range(3)]
+    assert m.batch(frames).is_complete()
+    assert m.batch(frames).csr("cpu").graph_kind == 1
+    assert m.batch(frames).csr("cpu", allow_complete=False).graph_kind == 0
+    assert not m.batch([m.complete_graph(5), m.complete_graph(4)]).is_complete()  # ragged
+    assert not m.frame_graph(rng.randn(6, 7), knn=3).is_complete()
+    assert m.batch([m.complete_graph(1), m.complete_graph(1)]).is_complete()
+    # same edge set, different edge order -> not the arithmetic numbering
+    s, d = m.complete_edges(4)
+    assert not m.graph((s[::-1], d[::-1]), num_nodes=4).is_complete()
