@@ -38,6 +38,7 @@
 namespace mrp {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr int kBlock = 256;  // threads per workgroup (4 waves)
 constexpr int kMaxChanPerBlock = 16;
@@ -77,6 +78,11 @@ __device__ __forceinline__ Frag<VEC> load_frag(const float* p) {
     f.v[1] = t.y;
     f.v[2] = t.z;
     f.v[3] = t.w;
+  } else if constexpr (VEC == 2) {
+    const f2* q = reinterpret_cast<const f2*>(p);
+    const f2 t = NTL ? __builtin_nontemporal_load(q) : *q;
+    f.v[0] = t.x;
+    f.v[1] = t.y;
   } else {
     f.v[0] = NTL ? __builtin_nontemporal_load(p) : *p;
   }
@@ -95,6 +101,14 @@ __device__ __forceinline__ void store_frag(float* p, const Frag<VEC>& f) {
       __builtin_nontemporal_store(t, reinterpret_cast<f4*>(p));
     else
       *reinterpret_cast<f4*>(p) = t;
+  } else if constexpr (VEC == 2) {
+    f2 t;
+    t.x = f.v[0];
+    t.y = f.v[1];
+    if (NTL)
+      __builtin_nontemporal_store(t, reinterpret_cast<f2*>(p));
+    else
+      *reinterpret_cast<f2*>(p) = t;
   } else {
     if (NTL)
       __builtin_nontemporal_store(f.v[0], p);
@@ -150,21 +164,32 @@ __device__ __forceinline__ void build_tiles_csr(const AggArgs& a, int node0, int
       float s = 1.f;
       if (BWD && a.mode != MRP_AGG_FILM_SUM && deg > 0) s = 1.f / (float)deg;
       unsigned mask = 0u;
-      for (int k = beg; k < end; ++k) {
-        const int u = a.src[k] - node0;
-        if ((unsigned)u >= (unsigned)n) continue;  // edge leaves the graph: rejected on the host
-        mask |= 1u << u;
-        float gam = 1.f, bet = 0.f;
-        if (a.mode != MRP_AGG_COPY_MEAN) {
-          const float* q = a.gb + ((int64_t)a.eid[k] * a.C + c) * 2;
-          gam = q[0];
-          bet = q[1];
+      // In-edges in chunks of KC, every load of a chunk issued before any is consumed (indices
+      // clamped instead of branched around, so the loads stay independent); accumulation stays
+      // in CSR order, so multi-edges sum deterministically.
+      constexpr int KC = NT < 8 ? NT : 8;  // edges per chunk (bounded: the first slice's loads are live here)
+      for (int k0 = beg; k0 < end; k0 += KC) {
+        int us[KC];
+        float2 gbv[KC];
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+          const int k = min(k0 + i, end - 1);
+          us[i] = a.src[k] - node0;
+          gbv[i] = a.mode != MRP_AGG_COPY_MEAN
+                       ? *reinterpret_cast<const float2*>(a.gb + ((int64_t)a.eid[k] * a.C + c) * 2)
+                       : make_float2(1.f, 0.f);
         }
-        if (BWD) {
-          Ga[cl * SZ + u * NTP + v] += s * gam;
-        } else {
-          Ga[cl * SZ + v * NTP + u] += gam;
-          Gb[cl * SZ + v * NTP + u] += bet;
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+          const int u = us[i];
+          if (k0 + i >= end || (unsigned)u >= (unsigned)n) continue;  // past v's list / leaves the graph
+          mask |= 1u << u;
+          if (BWD) {
+            Ga[cl * SZ + u * NTP + v] += s * gbv[i].x;
+          } else {
+            Ga[cl * SZ + v * NTP + u] += gbv[i].x;
+            Gb[cl * SZ + v * NTP + u] += gbv[i].y;
+          }
         }
       }
       if (cl == 0) {
@@ -431,9 +456,12 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
   }
 }
 
-// Reduce a value over the lpc lanes of one channel group (lpc is a power of two).
+// Reduce a value over the lpc lanes of one channel group (lpc is a power of two <= 64).  The six
+// butterfly steps are unrolled; the ones wider than the group are skipped by a uniform branch.
 __device__ __forceinline__ float group_sum(float x, int lpc) {
-  for (int m = lpc >> 1; m > 0; m >>= 1) x += __shfl_xor(x, m, 64);
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1)
+    if (m < lpc) x += __shfl_xor(x, m, 64);
   return x;
 }
 
@@ -444,8 +472,8 @@ __device__ __forceinline__ float group_sum(float x, int lpc) {
 //   grad_gb[e, c] = (s_v * D[v][u], s_v * S[v])    for every edge e = (u -> v).
 // For NT > 8 the kernel runs with VB = 4 and loops over destination blocks (x re-read from L2).
 // ---------------------------------------------------------------------------
-template <int NT, int VB, int VEC, bool COMPLETE>
-__global__ void __launch_bounds__(kBlock) film_bwd_fused(AggArgs a) {
+template <int NT, int VB, int VEC, bool COMPLETE, int MINW = 1>
+__global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
   constexpr bool kOnePass = VB == NT;
@@ -633,9 +661,9 @@ struct Geometry {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-Geometry make_geometry(int C, int P, bool vec4) {
+Geometry make_geometry(int C, int P, int vec) {
   Geometry g;
-  g.vec = vec4 ? 4 : 1;
+  g.vec = vec;
   const int pv = P / g.vec;
   int lpc = 1;
   while (lpc * 2 <= pv && lpc * 2 <= 64) lpc *= 2;
@@ -682,6 +710,8 @@ hipError_t launch_bwd_nt(const AggArgs& a_in, const Geometry& g, hipStream_t st)
     const size_t lds = lds_bwd<NT>(g.cpb);
     if (g.vec == 4)
       MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 4, COMPLETE>), lds);
+    else if (g.vec == 2)
+      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 2, COMPLETE>), lds);
     else
       MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 1, COMPLETE>), lds);
     return hipGetLastError();
@@ -691,6 +721,8 @@ hipError_t launch_bwd_nt(const AggArgs& a_in, const Geometry& g, hipStream_t st)
       const size_t lds = lds_dx<NT>(g.cpb);
       if (g.vec == 4)
         MRP_LAUNCH((mrp::film_bwd_dx<NT, 4, COMPLETE>), lds);
+      else if (g.vec == 2)
+        MRP_LAUNCH((mrp::film_bwd_dx<NT, 2, COMPLETE>), lds);
       else
         MRP_LAUNCH((mrp::film_bwd_dx<NT, 1, COMPLETE>), lds);
       hipError_t e = hipGetLastError();
@@ -702,6 +734,8 @@ hipError_t launch_bwd_nt(const AggArgs& a_in, const Geometry& g, hipStream_t st)
       const size_t lds = lds_bwd<NT>(g.cpb);
       if (g.vec == 4)
         MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 4, COMPLETE>), lds);
+      else if (g.vec == 2)
+        MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 2, COMPLETE>), lds);
       else
         MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 1, COMPLETE>), lds);
       return hipGetLastError();
@@ -780,7 +814,7 @@ int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, co
   if (mode != MRP_AGG_COPY_MEAN && num_edges > 0 && gb == nullptr) return hipErrorInvalidValue;
   const bool vec4 =
       (P % 4 == 0) && (x_node_stride % 4 == 0) && (out_node_stride % 4 == 0) && aligned16(x) && aligned16(out);
-  Geometry g = make_geometry(C, P, vec4);
+  Geometry g = make_geometry(C, P, vec4 ? 4 : 1);
   g.grid = (int64_t)num_graphs * g.ncb;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
   AggArgs a = {};
@@ -830,7 +864,11 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   bool vec4 = (P % 4 == 0) && (g_node_stride % 4 == 0) && aligned16(grad_out);
   if (want_dx) vec4 = vec4 && (gx_node_stride % 4 == 0) && aligned16(grad_x);
   if (want_dgb) vec4 = vec4 && (x_node_stride % 4 == 0) && aligned16(x);
-  Geometry g = make_geometry(C, P, vec4);
+  // With the Gram accumulators live (N >= 5 and d gamma/beta wanted), 16-byte slices cost
+  // occupancy (234 VGPRs at N=8); 8-byte slices keep 3 waves/SIMD and stream faster.
+  // (Measured on the complete-graph kernels; the CSR kernels keep 16-byte slices.)
+  const int vec = vec4 ? ((want_dgb && max_nodes >= 5 && graph_kind == MRP_GRAPH_COMPLETE) ? 2 : 4) : 1;
+  Geometry g = make_geometry(C, P, vec);
   g.grid = (int64_t)num_graphs * g.ncb;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
   AggArgs a = {};

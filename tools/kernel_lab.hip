@@ -257,6 +257,36 @@ int main(int argc, char** argv) {
     VAR(false, false, true, true, 1024)
     VAR(false, true, false, true, 1024)
   }
+  if (N == 8) {
+    // backward variants: slice width (VEC) and waves/SIMD bound
+    float* dgb;
+    CK(hipMalloc(&dgb, (size_t)E * C * 2 * 4));
+    const double bwd_bytes = (double)feat * 12 + (double)E * C * 2 * 8;
+    auto bargs = [&](int vec) {
+      mrp::AggArgs a = {};
+      a.x = x; a.xs = (int64_t)C * P; a.g = x; a.gs = (int64_t)C * P; a.gb = gb; a.goff = d_goff;
+      a.indptr = d_indptr; a.src = d_src; a.eid = d_eid; a.out = out; a.os = (int64_t)C * P; a.dgb = dgb;
+      a.C = C; a.P = P; a.PV = P / vec; a.mode = 0; a.lpc = 64; a.cpb = 4; a.ncb = C / 4;
+      a.want_dx = 1; a.want_dgb = 1;
+      return a;
+    };
+    const size_t lds = (size_t)(2 * 4 * mrp::Tile<8>::SZ + 4 * mrp::Tile<8>::NTP + mrp::Tile<8>::NTP) * 4;
+#define BVAR(VEC, MINW)                                                                                  \
+    {                                                                                                    \
+      mrp::AggArgs a = bargs(VEC);                                                                       \
+      float ms_ = time_ms([&] { hipLaunchKernelGGL((mrp::film_bwd_fused<8, 8, VEC, true, MINW>),         \
+                                                   dim3(B * a.ncb), dim3(256), lds, 0, a); }, iters);    \
+      char nm_[96];                                                                                      \
+      snprintf(nm_, sizeof nm_, "bwd_fused<8> vec=%d minw=%d", VEC, MINW);                              \
+      report(nm_, ms_, bwd_bytes);                                                                       \
+    }
+    BVAR(4, 1)
+    BVAR(4, 3)
+    BVAR(2, 1)
+    BVAR(2, 3)
+    BVAR(2, 4)
+    CK(hipFree(dgb));
+  }
   // product entry points (default geometry), both graph kinds
   for (int kind : {MRP_GRAPH_CSR, MRP_GRAPH_COMPLETE}) {
     char nm[96];
