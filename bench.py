@@ -119,6 +119,48 @@ def pmc_traffic(workload):
     return None, None
 
 
+def max_over_ranks(seconds, world, device, backend):
+    if world == 1:
+        return seconds
+    t = torch.tensor([seconds], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def train_step_time(gcn, g, x, world, device, args):
+    """One training step of the layer: forward, backward through the HIP kernels and the edge
+    encoder, and (N > 1) the bucketed gradient all-reduce of the replicated parameters."""
+    from mrp_gnn_amd.dist import GradAllReducer
+    xr = x.detach().clone().requires_grad_(True)
+    grad = torch.randn_like(x)
+    reducer = GradAllReducer(gcn.parameters()) if world > 1 else None
+
+    def step():
+        for p in gcn.parameters():
+            p.grad = None
+        xr.grad = None
+        gcn(g, xr).backward(grad)
+        if reducer is not None:
+            reducer.synchronize()
+
+    for _ in range(3):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.train_steps):
+        step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t = max_over_ranks((time.perf_counter() - t0) / args.train_steps, world, device, args.dist_backend)
+    nb = len(reducer.buckets) if reducer is not None else 0
+    if reducer is not None:
+        reducer.remove()
+    return t, nb
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -132,14 +174,20 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample-graphs", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-train", action="store_true", help="skip the training-step measurement")
+    ap.add_argument("--train-steps", type=int, default=20)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (control-flow tests)")
     args = ap.parse_args()
 
     rank, world, local = env_rank_world()
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local if world > 1 else 0)
+    ndev = max(torch.cuda.device_count(), 1)
+    device = torch.device("cuda", local % ndev)
     torch.cuda.set_device(device)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     B, N, C, H, W = args.graphs, args.nodes, args.channels, args.hw, args.hw
     P = H * W
@@ -168,15 +216,16 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, world, device, args.dist_backend)
 
         # dominant kernel alone, for the roofline
         gb = gcn.edge_encoder.film_params(g.edata["pose"])
         out = torch.empty_like(x)
         t_kernel = time_kernel(x, gb, csr, out, args.kernel_iters, device)
+
+    train = None
+    if not args.no_train:
+        train = train_step_time(gcn, g, x, world, device, args)
 
     elems_per_step = Nt * C * P
     value = world * elems_per_step * args.steps / elapsed
@@ -205,6 +254,14 @@ def main():
                      "read_frac": (bytes_launch - Nt * C * P * 4) / t_kernel / 1e9 / HBM_PEAK_GBS,
                      "traffic_source": traffic_src},
     }
+    if train is not None:
+        t_train, reducer_buckets = train
+        result["train_step"] = {
+            "what": "GCN layer forward + backward (HIP fused dx/dgamma/dbeta kernel, encoder backward)"
+                    + (" + bucketed gradient all-reduce" if world > 1 else ""),
+            "value": world * elems_per_step / t_train, "unit": "elems/s", "ms_per_step": t_train * 1e3,
+            "allreduce_buckets": reducer_buckets,
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(N, C, H, W, args.cpu_seconds, args.cpu_sample_graphs)
     if rank == 0:

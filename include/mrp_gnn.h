@@ -111,6 +111,20 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride,
                       float* grad_gb,
                       void* stream);
 
+/*
+ * Fused edge encoder (FiLM parameter generator), replacing edge_encoder.forward,
+ * dgl/model/models.py:146-154:  out = sigmoid(W2 relu(W1 pose + b1) + b2), i.e.
+ * Linear(9,C) -> ReLU -> Linear(C,2C) -> Sigmoid, in one kernel (fp32 MFMA for the second Linear,
+ * hidden activations kept on chip).  out (num_edges, 2C) row-major is the interleaved
+ * (num_edges, C, 2) gamma/beta tensor mrp_film_mean_fwd reads.
+ *
+ *   pose (num_edges, 9), w1 (C, 9), b1 (C), w2 (2C, C), b2 (2C): fp32, contiguous (torch
+ *   nn.Linear weight layout: [out_features, in_features]).
+ */
+int mrp_edge_encoder_fwd(const float* pose, const float* w1, const float* b1,
+                         const float* w2, const float* b2,
+                         int32_t num_edges, int32_t C, float* out, void* stream);
+
 /* Library identification: ABI version (incremented on signature changes). */
 int mrp_abi_version(void);
 

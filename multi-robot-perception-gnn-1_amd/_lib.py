@@ -21,10 +21,11 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
 EXPORTED_SYMBOLS = (
     "mrp_film_mean_fwd",
     "mrp_film_mean_bwd",
+    "mrp_edge_encoder_fwd",
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_NODES = 16
 
 MODE_FILM_MEAN = 0
@@ -48,6 +49,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_film_mean_fwd.restype = ctypes.c_int
     lib.mrp_film_mean_bwd.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _P]
     lib.mrp_film_mean_bwd.restype = ctypes.c_int
+    lib.mrp_edge_encoder_fwd.argtypes = [_P, _P, _P, _P, _P, _I32, _I32, _P, _P]
+    lib.mrp_edge_encoder_fwd.restype = ctypes.c_int
     lib.mrp_abi_version.argtypes = []
     lib.mrp_abi_version.restype = ctypes.c_int
     lib.mrp_error_string.argtypes = [ctypes.c_int]

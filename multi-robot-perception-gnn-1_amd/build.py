@@ -9,7 +9,7 @@ import sys
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
-SOURCES = [os.path.join(PKG_DIR, "csrc", "film_mean.hip")]
+SOURCES = [os.path.join(PKG_DIR, "csrc", "film_mean.hip"), os.path.join(PKG_DIR, "csrc", "edge_encoder.hip")]
 OUT = os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
 ARCH = os.environ.get("MRP_OFFLOAD_ARCH", "gfx950")
 

@@ -796,7 +796,7 @@ bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* ei
 
 extern "C" {
 
-int mrp_abi_version(void) { return 2; }
+int mrp_abi_version(void) { return 3; }
 
 const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
 

@@ -28,14 +28,16 @@ import torch
 import torch.nn as nn
 
 from .aggregate import film_mean
+from .encoder import fused_film_params
 
 
 class edge_encoder(nn.Module):  # noqa: N801  (reference class name)
     """FiLM parameter generator, ``dgl/model/models.py:142-155``."""
 
-    def __init__(self, layers_dim):
+    def __init__(self, layers_dim, fused: bool = True):
         super().__init__()
         self.layers_dim = layers_dim
+        self.fused = fused
         self.layers = nn.Sequential(
             nn.Linear(9, layers_dim[0]),
             nn.ReLU(),
@@ -44,7 +46,11 @@ class edge_encoder(nn.Module):  # noqa: N801  (reference class name)
         )
 
     def film_params(self, edge: torch.Tensor) -> torch.Tensor:
-        """Interleaved gamma/beta, (E, C, 2): the tensor the kernel reads in place."""
+        """Interleaved gamma/beta, (E, C, 2): the tensor the aggregation kernel reads in place.
+        On the GPU the whole Linear/ReLU/Linear/Sigmoid stack is one fused HIP kernel
+        (``mrp_edge_encoder_fwd``); on the CPU it is the reference's torch layers."""
+        if edge.is_cuda and self.fused:
+            return fused_film_params(self.layers, edge).view(-1, self.layers_dim[1], 2)
         return self.layers(edge.float()).view(-1, self.layers_dim[1], 2)
 
     def forward(self, edge: torch.Tensor):
