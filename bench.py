@@ -5,8 +5,8 @@ Workload (SURVEY.md §8(d) north-star target): per rank B=32 per-frame graphs of
 (complete directed graphs, the reference's ``dgl/dataloader.py:88-95``), node features
 C=512 x 32 x 32 fp32 (ResNet18 width at H/8 x W/8 of a 256^2 image), synthetic and seeded, already
 resident in HBM.  A *step* is one forward pass of the drop-in ``GCN`` layer over that batch:
-edge encoder (9 -> C -> 2C Linear/ReLU/Linear/Sigmoid on the 1792 edge poses) + the HIP FiLM-mean
-aggregation.  value = elements (Nt*C*H*W) aggregated per second over all ranks.
+edge encoder (9 -> C -> 2C Linear/ReLU/Linear/Sigmoid on the 1792 edge poses: HIP hidden-layer
+kernel + library GEMM) + the HIP FiLM-mean aggregation (which applies the encoder's sigmoid).  value = elements (Nt*C*H*W) aggregated per second over all ranks.
 
 Multi-GPU (``torch.distributed.run``, one process per GPU): graphs of a batch are independent, so
 each rank runs its own B=32 graphs with no data-path collective ("scaling": "weak"); time is the
@@ -66,14 +66,15 @@ def alg_bytes_fwd(Nt, E, C, P):
 def time_kernel(x, gb, csr, out, iters, device):
     """Mean duration of one aggregation launch, HIP events on the launch stream."""
     stream = torch.cuda.current_stream(device)
+    mode = mrp._lib.MODE_FILM_MEAN | mrp._lib.GB_LOGITS
     for _ in range(3):
-        mrp.film_mean_forward_into(x, gb, csr, 0, out)
+        mrp.film_mean_forward_into(x, gb, csr, mode, out)
     start = torch.cuda.Event(enable_timing=True)
     end = torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(device)
     start.record(stream)
     for _ in range(iters):
-        mrp.film_mean_forward_into(x, gb, csr, 0, out)
+        mrp.film_mean_forward_into(x, gb, csr, mode, out)
     end.record(stream)
     end.synchronize()
     return start.elapsed_time(end) / iters * 1e-3  # seconds
@@ -219,9 +220,9 @@ def main():
         elapsed = max_over_ranks(elapsed, world, device, args.dist_backend)
 
         # dominant kernel alone, for the roofline
-        gb = gcn.edge_encoder.film_params(g.edata["pose"])
+        z = gcn.edge_encoder.logits(g.edata["pose"])  # what GCN.forward hands the kernel
         out = torch.empty_like(x)
-        t_kernel = time_kernel(x, gb, csr, out, args.kernel_iters, device)
+        t_kernel = time_kernel(x, z, csr, out, args.kernel_iters, device)
 
     train = None
     if not args.no_train:

@@ -64,6 +64,12 @@ enum mrp_agg_mode {
                               dgl_models.py:126 ("multi_view_dgl_mean_wofilm")         */
 };
 
+/* Flag OR-ed into `mode`: gb holds the edge encoder's pre-sigmoid logits z (the output of its
+ * second Linear); the kernels apply gamma/beta = sigmoid(z) while building their tiles (forward)
+ * and return d z = d gamma/beta * s (1 - s) (backward).  Fuses the encoder's Sigmoid
+ * (dgl/model/models.py:150) into the aggregation. */
+#define MRP_AGG_GB_LOGITS 0x100
+
 /*
  * Forward: out[v] = reduce over in-edges e=(u->v) of (gamma_e (.) x[u] + beta_e).
  * Replaces g.update_all(edge_udf, node_udf), dgl/model/models.py:223.
@@ -112,18 +118,13 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride,
                       void* stream);
 
 /*
- * Fused edge encoder (FiLM parameter generator), replacing edge_encoder.forward,
- * dgl/model/models.py:146-154:  out = sigmoid(W2 relu(W1 pose + b1) + b2), i.e.
- * Linear(9,C) -> ReLU -> Linear(C,2C) -> Sigmoid, in one kernel (fp32 MFMA for the second Linear,
- * hidden activations kept on chip).  out (num_edges, 2C) row-major is the interleaved
- * (num_edges, C, 2) gamma/beta tensor mrp_film_mean_fwd reads.
- *
- *   pose (num_edges, 9), w1 (C, 9), b1 (C), w2 (2C, C), b2 (2C): fp32, contiguous (torch
- *   nn.Linear weight layout: [out_features, in_features]).
+ * First layer of the edge encoder, dgl/model/models.py:147-148:  h = relu(pose W1^T + b1).
+ *   pose (num_edges, 9), w1 (C, 9) (nn.Linear weight layout), b1 (C) -> h (num_edges, C), fp32.
+ * The second Linear is a plain library GEMM and its Sigmoid is fused into the aggregation
+ * (MRP_AGG_GB_LOGITS).
  */
-int mrp_edge_encoder_fwd(const float* pose, const float* w1, const float* b1,
-                         const float* w2, const float* b2,
-                         int32_t num_edges, int32_t C, float* out, void* stream);
+int mrp_edge_hidden_fwd(const float* pose, const float* w1, const float* b1,
+                        int32_t num_edges, int32_t C, float* h, void* stream);
 
 /* Library identification: ABI version (incremented on signature changes). */
 int mrp_abi_version(void);

@@ -21,16 +21,17 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
 EXPORTED_SYMBOLS = (
     "mrp_film_mean_fwd",
     "mrp_film_mean_bwd",
-    "mrp_edge_encoder_fwd",
+    "mrp_edge_hidden_fwd",
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_NODES = 16
 
 MODE_FILM_MEAN = 0
 MODE_FILM_SUM = 1
 MODE_COPY_MEAN = 2
+GB_LOGITS = 0x100  # mode flag: gb holds pre-sigmoid logits
 GRAPH_CSR = 0
 GRAPH_COMPLETE = 1
 MODES = {"film_mean": MODE_FILM_MEAN, "film_sum": MODE_FILM_SUM, "copy_mean": MODE_COPY_MEAN}
@@ -49,8 +50,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_film_mean_fwd.restype = ctypes.c_int
     lib.mrp_film_mean_bwd.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _P]
     lib.mrp_film_mean_bwd.restype = ctypes.c_int
-    lib.mrp_edge_encoder_fwd.argtypes = [_P, _P, _P, _P, _P, _I32, _I32, _P, _P]
-    lib.mrp_edge_encoder_fwd.restype = ctypes.c_int
+    lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
+    lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
     lib.mrp_abi_version.argtypes = []
     lib.mrp_abi_version.restype = ctypes.c_int
     lib.mrp_error_string.argtypes = [ctypes.c_int]

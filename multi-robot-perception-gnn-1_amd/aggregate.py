@@ -69,7 +69,7 @@ def film_mean_forward_into(x: torch.Tensor, gb: Optional[torch.Tensor], csr: Gra
     os_ = node_stride(out)
     if os_ is None or tuple(out.shape) != (n, C, H, W):
         raise ValueError("out must be (N, C, H, W) fp32 with a contiguous C*H*W block per node")
-    if mode != _lib.MODE_COPY_MEAN:
+    if (mode & ~_lib.GB_LOGITS) != _lib.MODE_COPY_MEAN:
         if gb is None:
             raise ValueError("gamma/beta tensor required for FiLM modes")
         gb = gb.reshape(csr.num_edges, C, 2)
@@ -99,7 +99,7 @@ def film_mean_backward(grad_out: torch.Tensor, x: torch.Tensor, gb: Optional[tor
     dx = torch.empty((n, C, H, W), device=x.device, dtype=torch.float32) if need_dx else None
     dgb = torch.empty((csr.num_edges, C, 2), device=x.device, dtype=torch.float32) if need_dgb else None
     xs = 0
-    if need_dgb and mode != _lib.MODE_COPY_MEAN:
+    if need_dgb and (mode & ~_lib.GB_LOGITS) != _lib.MODE_COPY_MEAN:
         x, xs = _as_node_major(x)
     if gb is not None:
         gb = gb.reshape(csr.num_edges, C, 2)
@@ -117,7 +117,8 @@ def film_mean_backward(grad_out: torch.Tensor, x: torch.Tensor, gb: Optional[tor
 
 
 class FilmMeanFunction(torch.autograd.Function):
-    """Autograd wrapper: forward = ``mrp_film_mean_fwd``, backward = ``mrp_film_mean_bwd``."""
+    """Autograd wrapper: forward = ``mrp_film_mean_fwd``, backward = ``mrp_film_mean_bwd``.
+    ``mode`` may carry ``_lib.GB_LOGITS`` (gb = pre-sigmoid logits; the gradient is then d logits)."""
 
     @staticmethod
     def forward(ctx, x, gb, csr: GraphCSR, mode: int):
@@ -139,11 +140,13 @@ class FilmMeanFunction(torch.autograd.Function):
         return dx, dgb, None, None
 
 
-def film_mean(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="film_mean") -> torch.Tensor:
+def film_mean(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="film_mean",
+              logits: bool = False) -> torch.Tensor:
     """``mean_e(gamma_e * x_src + beta_e)`` per destination node (see module docstring).
 
     x: (N, C, H, W) fp32 on a ROCm device; gb: (E, 2C) or (E, C, 2) interleaved gamma/beta
-    (ignored for ``mode='copy_mean'``); csr: ``RobotGraph.csr(device)``.
+    (ignored for ``mode='copy_mean'``), or their pre-sigmoid logits with ``logits=True`` (the
+    encoder's Sigmoid then runs inside the kernel); csr: ``RobotGraph.csr(device)``.
     """
     m = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
     if x.dim() != 4:
@@ -153,4 +156,6 @@ def film_mean(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="
     _require_device(x)
     if m == _lib.MODE_COPY_MEAN:
         gb = None
+    elif logits:
+        m |= _lib.GB_LOGITS
     return FilmMeanFunction.apply(x, gb, csr, m)

@@ -61,7 +61,16 @@ struct AggArgs {
   int32_t cpb;  // channels per workgroup
   int32_t ncb;  // channel blocks per graph
   int32_t want_dx, want_dgb;
+  int32_t logits;  // gb holds pre-sigmoid logits (MRP_AGG_GB_LOGITS): apply sigmoid on load
 };
+
+__device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
+
+// d/dz of gamma/beta = sigmoid(z): grad * s * (1 - s)
+__device__ __forceinline__ float2 sigmoid_backward(float2 grad, float2 z) {
+  const float sg = sigmoidf(z.x), sb = sigmoidf(z.y);
+  return make_float2(grad.x * sg * (1.f - sg), grad.y * sb * (1.f - sb));
+}
 
 template <int VEC>
 struct Frag {
@@ -179,6 +188,10 @@ __device__ __forceinline__ void build_tiles_csr(const AggArgs& a, int node0, int
                        ? *reinterpret_cast<const float2*>(a.gb + ((int64_t)a.eid[k] * a.C + c) * 2)
                        : make_float2(1.f, 0.f);
         }
+        if (a.logits && a.mode != MRP_AGG_COPY_MEAN) {
+#pragma unroll
+          for (int i = 0; i < KC; ++i) gbv[i] = make_float2(sigmoidf(gbv[i].x), sigmoidf(gbv[i].y));
+        }
 #pragma unroll
         for (int i = 0; i < KC; ++i) {
           const int u = us[i];
@@ -235,6 +248,7 @@ __device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, 
           val = make_float2(1.f, 0.f);
         } else {
           val = *reinterpret_cast<const float2*>(a.gb + (complete_eid(ebase, NT, u, v) * a.C + c) * 2);
+          if (a.logits) val = make_float2(sigmoidf(val.x), sigmoidf(val.y));
         }
       }
     }
@@ -616,8 +630,10 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
       const int v = slot / NT, u = slot - v * NT;
       const int cc = c0 + cl;
       if (u == v || cc >= a.C) continue;
-      const float2 r = make_float2(s * Dl[cl * SZ + v * NTP + u], s * Sl[cl * NTP + v]);
-      *reinterpret_cast<float2*>(a.dgb + (complete_eid(ebase, NT, u, v) * a.C + cc) * 2) = r;
+      float2 r = make_float2(s * Dl[cl * SZ + v * NTP + u], s * Sl[cl * NTP + v]);
+      const int64_t off = (complete_eid(ebase, NT, u, v) * a.C + cc) * 2;
+      if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
+      *reinterpret_cast<float2*>(a.dgb + off) = r;
     }
     return;
   }
@@ -640,7 +656,10 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
         dgam = s * Dl[cl * SZ + v * NTP + u];
         dbet = dbeta;
       }
-      *reinterpret_cast<float2*>(a.dgb + ((int64_t)a.eid[k] * a.C + cc) * 2) = make_float2(dgam, dbet);
+      const int64_t off = ((int64_t)a.eid[k] * a.C + cc) * 2;
+      float2 r = make_float2(dgam, dbet);
+      if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
+      *reinterpret_cast<float2*>(a.dgb + off) = r;
     }
   }
 }
@@ -796,14 +815,16 @@ bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* ei
 
 extern "C" {
 
-int mrp_abi_version(void) { return 3; }
+int mrp_abi_version(void) { return 4; }
 
 const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
 
 int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr,
                       const int32_t* src, const int32_t* eid, const int32_t* graph_off, int32_t num_graphs,
                       int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C,
-                      int32_t P, int32_t mode, float* out, int64_t out_node_stride, void* stream) {
+                      int32_t P, int32_t mode_flags, float* out, int64_t out_node_stride, void* stream) {
+  const int32_t logits = (mode_flags & MRP_AGG_GB_LOGITS) ? 1 : 0;
+  const int32_t mode = mode_flags & ~MRP_AGG_GB_LOGITS;
   if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind, num_nodes, num_edges, C, P,
                       mode))
     return hipErrorInvalidValue;
@@ -834,14 +855,17 @@ int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, co
   a.lpc = g.lpc;
   a.cpb = g.cpb;
   a.ncb = g.ncb;
+  a.logits = logits;
   return dispatch_fwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, static_cast<hipStream_t>(stream));
 }
 
 int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float* x, int64_t x_node_stride,
                       const float* gb, const int32_t* indptr, const int32_t* src, const int32_t* eid,
                       const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
-                      int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode, float* grad_x,
+                      int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode_flags, float* grad_x,
                       int64_t gx_node_stride, float* grad_gb, void* stream) {
+  const int32_t logits = (mode_flags & MRP_AGG_GB_LOGITS) ? 1 : 0;
+  const int32_t mode = mode_flags & ~MRP_AGG_GB_LOGITS;
   if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind, num_nodes, num_edges, C, P,
                       mode))
     return hipErrorInvalidValue;
@@ -893,6 +917,7 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   a.ncb = g.ncb;
   a.want_dx = want_dx ? 1 : 0;
   a.want_dgb = want_dgb ? 1 : 0;
+  a.logits = logits;
   return dispatch_bwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, st);
 }
 

@@ -28,16 +28,15 @@ import torch
 import torch.nn as nn
 
 from .aggregate import film_mean
-from .encoder import fused_film_params
+from .encoder import edge_logits
 
 
 class edge_encoder(nn.Module):  # noqa: N801  (reference class name)
     """FiLM parameter generator, ``dgl/model/models.py:142-155``."""
 
-    def __init__(self, layers_dim, fused: bool = True):
+    def __init__(self, layers_dim):
         super().__init__()
         self.layers_dim = layers_dim
-        self.fused = fused
         self.layers = nn.Sequential(
             nn.Linear(9, layers_dim[0]),
             nn.ReLU(),
@@ -45,13 +44,19 @@ class edge_encoder(nn.Module):  # noqa: N801  (reference class name)
             nn.Sigmoid(),
         )
 
+    def logits(self, edge: torch.Tensor) -> torch.Tensor:
+        """Pre-sigmoid FiLM parameters z, (E, C, 2) interleaved.  On the GPU: the hidden layer is a
+        HIP kernel and the second Linear a library GEMM (``encoder.edge_logits``); the sigmoid is
+        left to the aggregation kernel (``MRP_AGG_GB_LOGITS``)."""
+        if edge.is_cuda:
+            z = edge_logits(self.layers, edge)
+        else:
+            z = self.layers[2](self.layers[1](self.layers[0](edge.float())))
+        return z.view(-1, self.layers_dim[1], 2)
+
     def film_params(self, edge: torch.Tensor) -> torch.Tensor:
-        """Interleaved gamma/beta, (E, C, 2): the tensor the aggregation kernel reads in place.
-        On the GPU the whole Linear/ReLU/Linear/Sigmoid stack is one fused HIP kernel
-        (``mrp_edge_encoder_fwd``); on the CPU it is the reference's torch layers."""
-        if edge.is_cuda and self.fused:
-            return fused_film_params(self.layers, edge).view(-1, self.layers_dim[1], 2)
-        return self.layers(edge.float()).view(-1, self.layers_dim[1], 2)
+        """Interleaved gamma/beta = sigmoid(z), (E, C, 2) (``models.py:153-154``)."""
+        return torch.sigmoid(self.logits(edge))
 
     def forward(self, edge: torch.Tensor):
         """Reference return value: gamma, beta as (E, C, 1, 1) views (``models.py:152-155``)."""
@@ -76,10 +81,11 @@ class GCN(nn.Module):
         if _opt(self.opt, "gcn_return", "aggregate") == "input":
             return x  # models.py:226 returns the input; update_all's result is never read
         mode = _opt(self.opt, "gcn_mode", "film_mean")
-        gb = None
-        if mode != "copy_mean":
-            gb = self.edge_encoder.film_params(g.edata["pose"])
-        return film_mean(x, gb, g.csr(x.device), mode)
+        if mode == "copy_mean":
+            return film_mean(x, None, g.csr(x.device), mode)
+        # logits in, sigmoid applied inside the aggregation kernel
+        z = self.edge_encoder.logits(g.edata["pose"])
+        return film_mean(x, z, g.csr(x.device), mode, logits=True)
 
 
 class GCNBlock(nn.Module):

@@ -1,5 +1,5 @@
-"""GPU: the fused edge encoder (mrp_edge_encoder_fwd) against the reference's torch layers and the
-golden fixtures; its autograd backward against torch autograd."""
+"""GPU: the edge encoder path (HIP hidden layer + library GEMM + sigmoid fused into the
+aggregation) against the reference's torch layers and the golden fixtures."""
 import numpy as np
 import pytest
 import torch
@@ -12,7 +12,7 @@ PARAM_KEYS = ["layers.0.weight", "layers.0.bias", "layers.2.weight", "layers.2.b
 
 
 @pytest.mark.parametrize("name", [n for n in golden_cases() if "copyu" not in n])
-def test_fused_encoder_matches_reference_fixture(cuda_device, name):
+def test_encoder_matches_reference_fixture(cuda_device, name):
     z = load_golden(name)
     C = z["x"].shape[1]
     enc = m.edge_encoder([C, C])
@@ -22,30 +22,49 @@ def test_fused_encoder_matches_reference_fixture(cuda_device, name):
     assert rel_err(gb.detach().cpu().numpy(), z["gb"]) <= 1e-5
 
 
-@pytest.mark.parametrize("E,C", [(1, 1), (7, 3), (96, 64), (1792, 512), (100, 130), (33, 1280), (448, 2048)])
-def test_fused_encoder_vs_torch_layers(cuda_device, E, C):
+@pytest.mark.parametrize("E,C", [(1, 1), (7, 3), (96, 64), (1792, 512), (100, 130), (33, 1281)])
+def test_hidden_kernel_vs_torch(cuda_device, E, C):
     torch.manual_seed(E + C)
     enc = m.edge_encoder([C, C]).to(cuda_device)
     pose = (torch.randn(E, 9) * 5).to(cuda_device)
-    fused = enc.film_params(pose)
-    ref = enc.layers(pose).view(E, C, 2)
-    assert fused.shape == ref.shape
-    assert float((fused - ref).abs().max()) <= 2e-6  # sigmoid outputs in (0, 1)
-    # backward: custom Function vs torch autograd through the same layers
-    g = torch.randn_like(ref)
+    l1 = enc.layers[0]
+    h = m.encoder.hidden_forward(pose, l1.weight, l1.bias)
+    ref = torch.relu(l1(pose))
+    assert float((h - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
+    # the full logits path and its backward vs torch autograd through the reference layers
+    g = torch.randn(E, 2 * C, device=cuda_device)
     pr = pose.clone().requires_grad_(True)
     pf = pose.clone().requires_grad_(True)
     enc.zero_grad()
-    (enc.layers(pr).view(E, C, 2) * g).sum().backward()
+    (enc.layers[2](torch.relu(enc.layers[0](pr))) * g).sum().backward()
     ref_grads = [p.grad.clone() for p in enc.parameters()] + [pr.grad.clone()]
     enc.zero_grad()
-    (enc.film_params(pf) * g).sum().backward()
+    zl = enc.logits(pf).reshape(E, 2 * C)
+    assert rel_err(zl.detach().cpu().numpy(), enc.layers[2](torch.relu(enc.layers[0](pose))).detach().cpu().numpy()) <= 1e-5
+    (zl * g).sum().backward()
     got_grads = [p.grad.clone() for p in enc.parameters()] + [pf.grad.clone()]
     for a, b in zip(got_grads, ref_grads):
         assert rel_err(a.cpu().numpy(), b.cpu().numpy()) <= 1e-4
 
 
-def test_fused_encoder_empty(cuda_device):
-    enc = m.edge_encoder([8, 8]).to(cuda_device)
-    out = enc.film_params(torch.zeros(0, 9, device=cuda_device))
-    assert out.shape == (0, 8, 2)
+@pytest.mark.parametrize("complete", [True, False])
+@pytest.mark.parametrize("n", [3, 8, 12])
+def test_logits_fusion_equals_explicit_sigmoid(cuda_device, complete, n):
+    """film_mean(x, z, logits=True) == film_mean(x, sigmoid(z)) and its gradient w.r.t. z equals
+    the chain rule through torch.sigmoid."""
+    rng = np.random.RandomState(n)
+    graphs = [m.frame_graph(np.concatenate([rng.uniform(-5, 5, (n, 3)), rng.randn(n, 4)], 1)) for _ in range(3)]
+    g = m.batch(graphs)
+    csr = g.csr(cuda_device, allow_complete=complete)
+    torch.manual_seed(n)
+    x = torch.randn(g.num_nodes(), 16, 8, 8, device=cuda_device)
+    zl = (torch.randn(g.num_edges(), 16, 2) * 3).to(cuda_device)
+    G = torch.randn_like(x)
+    z1 = zl.clone().requires_grad_(True)
+    z2 = zl.clone().requires_grad_(True)
+    a = m.film_mean(x, z1, csr, logits=True)
+    b = m.film_mean(x, torch.sigmoid(z2), csr)
+    assert rel_err(a.detach().cpu().numpy(), b.detach().cpu().numpy()) <= 1e-6
+    a.backward(G)
+    b.backward(G)
+    assert rel_err(z1.grad.cpu().numpy(), z2.grad.cpu().numpy()) <= 1e-5

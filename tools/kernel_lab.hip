@@ -7,6 +7,7 @@
 //   film_fwd<N,4> : the product kernel at several (lanes-per-channel, channels-per-block) geometries
 // Usage: kernel_lab [B N C HW iters]
 #include "../multi-robot-perception-gnn-1_amd/csrc/film_mean.hip"
+#include "../multi-robot-perception-gnn-1_amd/csrc/edge_encoder.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -169,9 +170,10 @@ int main(int argc, char** argv) {
   indptr[Nt] = k;
   goff[B] = Nt;
   const size_t feat = (size_t)Nt * C * P;
-  float *x, *out, *gb;
+  float *x, *out, *gb, *gout;
   int *d_indptr, *d_src, *d_eid, *d_goff;
   CK(hipMalloc(&x, feat * 4));
+  CK(hipMalloc(&gout, feat * 4));  // backward's grad_out: its own buffer (aliasing x would hit cache)
   CK(hipMalloc(&out, feat * 4));
   CK(hipMalloc(&gb, (size_t)E * C * 2 * 4));
   CK(hipMalloc(&d_indptr, (Nt + 1) * 4));
@@ -186,6 +188,8 @@ int main(int argc, char** argv) {
     std::vector<float> h(feat);
     for (size_t i = 0; i < feat; ++i) h[i] = (float)((i * 2654435761u) % 1000) / 500.f - 1.f;
     CK(hipMemcpy(x, h.data(), feat * 4, hipMemcpyHostToDevice));
+    for (size_t i = 0; i < feat; ++i) h[i] = (float)((i * 97u) % 1000) / 500.f - 1.f;
+    CK(hipMemcpy(gout, h.data(), feat * 4, hipMemcpyHostToDevice));
     std::vector<float> hg((size_t)E * C * 2);
     for (size_t i = 0; i < hg.size(); ++i) hg[i] = (float)((i * 40503u) % 1000) / 1000.f;
     CK(hipMemcpy(gb, hg.data(), hg.size() * 4, hipMemcpyHostToDevice));
@@ -264,7 +268,7 @@ int main(int argc, char** argv) {
     const double bwd_bytes = (double)feat * 12 + (double)E * C * 2 * 8;
     auto bargs = [&](int vec) {
       mrp::AggArgs a = {};
-      a.x = x; a.xs = (int64_t)C * P; a.g = x; a.gs = (int64_t)C * P; a.gb = gb; a.goff = d_goff;
+      a.x = x; a.xs = (int64_t)C * P; a.g = gout; a.gs = (int64_t)C * P; a.gb = gb; a.goff = d_goff;
       a.indptr = d_indptr; a.src = d_src; a.eid = d_eid; a.out = out; a.os = (int64_t)C * P; a.dgb = dgb;
       a.C = C; a.P = P; a.PV = P / vec; a.mode = 0; a.lpc = 64; a.cpb = 4; a.ncb = C / 4;
       a.want_dx = 1; a.want_dgb = 1;
@@ -297,12 +301,38 @@ int main(int argc, char** argv) {
     snprintf(nm, sizeof nm, "mrp_film_mean_fwd kind=%s", kind ? "complete" : "csr");
     report(nm, ms, alg);
     ms = time_ms([&] {
-      CK((hipError_t)mrp_film_mean_bwd(x, (int64_t)C * P, x, (int64_t)C * P, gb, d_indptr, d_src, d_eid, d_goff, B,
+      CK((hipError_t)mrp_film_mean_bwd(gout, (int64_t)C * P, x, (int64_t)C * P, gb, d_indptr, d_src, d_eid, d_goff, B,
                                        N, kind, Nt, E, C, P, 0, out, (int64_t)C * P, gb, nullptr));
     }, iters);
     snprintf(nm, sizeof nm, "mrp_film_mean_bwd kind=%s (dx+dgb)", kind ? "complete" : "csr");
     // bwd alg bytes: read G and x, write dx, read gb, write dgb
     report(nm, ms, (double)feat * 12 + (double)E * C * 2 * 8);
+  }
+  {
+    // fused edge encoder on the same E edges (C -> 2C)
+    float *pose, *w1, *b1, *w2, *b2, *eo;
+    CK(hipMalloc(&pose, (size_t)E * 9 * 4));
+    CK(hipMalloc(&w1, (size_t)C * 9 * 4));
+    CK(hipMalloc(&b1, (size_t)C * 4));
+    CK(hipMalloc(&w2, (size_t)2 * C * C * 4));
+    CK(hipMalloc(&b2, (size_t)2 * C * 4));
+    CK(hipMalloc(&eo, (size_t)E * 2 * C * 4));
+    auto fill = [](float* d, size_t n, float scale) {  // random data: MFMA clocks differ on zeros
+      std::vector<float> h(n);
+      uint32_t s = 12345u;
+      for (auto& v : h) { s = s * 1664525u + 1013904223u; v = scale * ((float)(s >> 8) / 16777216.f - 0.5f); }
+      CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+    };
+    fill(pose, (size_t)E * 9, 10.f);
+    fill(w1, (size_t)C * 9, 0.6f);
+    fill(b1, (size_t)C, 0.6f);
+    fill(w2, (size_t)2 * C * C, 0.08f);
+    fill(b2, (size_t)2 * C, 0.08f);
+    float ms = time_ms([&] { CK((hipError_t)mrp_edge_encoder_fwd(pose, w1, b1, w2, b2, E, C, eo, nullptr)); }, iters);
+    const double flops = 2.0 * E * (9.0 * C + 2.0 * C * C);
+    printf("%-40s %9.1f us  %7.1f TFLOP/s  %5.1f%% of 157 TF fp32\n", "mrp_edge_encoder_fwd", ms * 1e3,
+           flops / ms / 1e9, flops / ms / 1e9 / 157.3 * 100);
+    CK(hipFree(pose)); CK(hipFree(w1)); CK(hipFree(b1)); CK(hipFree(w2)); CK(hipFree(b2)); CK(hipFree(eo));
   }
   CK(hipFree(x));
   CK(hipFree(out));
