@@ -104,6 +104,9 @@ int mrp_film_mean_fwd(const float* x, int64_t x_node_stride,
  *
  * grad_x (node stride gx_node_stride) and grad_gb ((num_edges, C, 2), interleaved
  * like gb) may each be NULL to skip that output.  For COPY_MEAN grad_gb is zero-filled.
+ * grad_x_base (node stride base_node_stride, may be NULL) is added to grad_x: the backward of
+ * torch.cat((x, out), 1) (dgl/model/models.py:182) passes the first half of the concatenation's
+ * gradient here and the second half as grad_out, so x's total gradient is one pass.
  * Deterministic: no atomics; each output element is written by exactly one lane.
  */
 int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride,
@@ -114,6 +117,7 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride,
                       int32_t graph_kind, int32_t num_nodes, int32_t num_edges,
                       int32_t C, int32_t P, int32_t mode,
                       float* grad_x, int64_t gx_node_stride,
+                      const float* grad_x_base, int64_t base_node_stride,
                       float* grad_gb,
                       void* stream);
 

@@ -25,7 +25,7 @@ EXPORTED_SYMBOLS = (
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_NODES = 16
 
 MODE_FILM_MEAN = 0
@@ -48,7 +48,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     graph = [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32]  # indptr..mode
     lib.mrp_film_mean_fwd.argtypes = [_P, _I64, _P] + graph + [_P, _I64, _P]
     lib.mrp_film_mean_fwd.restype = ctypes.c_int
-    lib.mrp_film_mean_bwd.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _P]
+    lib.mrp_film_mean_bwd.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _I64, _P, _P]
     lib.mrp_film_mean_bwd.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int

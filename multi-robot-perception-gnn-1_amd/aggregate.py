@@ -91,11 +91,15 @@ def film_mean_forward_into(x: torch.Tensor, gb: Optional[torch.Tensor], csr: Gra
 
 
 def film_mean_backward(grad_out: torch.Tensor, x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR,
-                       mode: int, need_dx: bool, need_dgb: bool):
-    """(grad_x or None, grad_gb (E, C, 2) or None) for the forward above."""
+                       mode: int, need_dx: bool, need_dgb: bool, grad_x_base: Optional[torch.Tensor] = None):
+    """(grad_x or None, grad_gb (E, C, 2) or None) for the forward above; ``grad_x_base`` (N, C, H, W),
+    if given, is added into grad_x by the kernel."""
     _require_device(grad_out, x)
     n, C, H, W = x.shape
     grad_out, gs = _as_node_major(grad_out)
+    bs = 0
+    if grad_x_base is not None:
+        grad_x_base, bs = _as_node_major(grad_x_base)
     dx = torch.empty((n, C, H, W), device=x.device, dtype=torch.float32) if need_dx else None
     dgb = torch.empty((csr.num_edges, C, 2), device=x.device, dtype=torch.float32) if need_dgb else None
     xs = 0
@@ -111,7 +115,7 @@ def film_mean_backward(grad_out: torch.Tensor, x: torch.Tensor, gb: Optional[tor
             _ptr(grad_out), gs, _ptr(x), xs, _ptr(gb), _ptr(csr.indptr), _ptr(csr.src), _ptr(csr.eid),
             _ptr(csr.graph_off), csr.num_graphs, csr.max_nodes, csr.graph_kind, csr.num_nodes, csr.num_edges, C,
             H * W, mode,
-            _ptr(dx), (C * H * W) if dx is not None else 0, _ptr(dgb), _stream(x.device))
+            _ptr(dx), (C * H * W) if dx is not None else 0, _ptr(grad_x_base), bs, _ptr(dgb), _stream(x.device))
     _lib.check(code, "mrp_film_mean_bwd")
     return dx, dgb
 
@@ -159,3 +163,47 @@ def film_mean(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="
     elif logits:
         m |= _lib.GB_LOGITS
     return FilmMeanFunction.apply(x, gb, csr, m)
+
+
+class FilmMeanCatFunction(torch.autograd.Function):
+    """``torch.cat((x, film_mean(x, gb)), 1)`` without the concatenation pass for the aggregate
+    (``dgl/model/models.py:181-182,187-188``): the kernel writes straight into the second half of the
+    (N, 2C, H, W) buffer; backward hands the kernel the second half of the incoming gradient as
+    grad_out and the first half as the base of x's gradient."""
+
+    @staticmethod
+    def forward(ctx, x, gb, csr: GraphCSR, mode: int):
+        n, C, H, W = x.shape
+        buf = torch.empty((n, 2 * C, H, W), device=x.device, dtype=torch.float32)
+        buf[:, :C].copy_(x)
+        film_mean_forward_into(x, gb, csr, mode, buf[:, C:])
+        ctx.save_for_backward(x, gb)
+        ctx.csr = csr
+        ctx.mode = mode
+        return buf
+
+    @staticmethod
+    def backward(ctx, grad_buf):
+        x, gb = ctx.saved_tensors
+        C = x.shape[1]
+        need_dx = ctx.needs_input_grad[0]
+        need_dgb = gb is not None and ctx.needs_input_grad[1]
+        dx, dgb = film_mean_backward(grad_buf[:, C:], x, gb, ctx.csr, ctx.mode, need_dx, need_dgb,
+                                     grad_x_base=grad_buf[:, :C] if need_dx else None)
+        if dgb is not None:
+            dgb = dgb.view(gb.shape)
+        return dx, dgb, None, None
+
+
+def film_mean_cat(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="film_mean",
+                  logits: bool = False) -> torch.Tensor:
+    """``torch.cat((x, film_mean(x, gb, csr, mode, logits)), dim=1)`` in one kernel pass."""
+    m = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
+    if x.dim() != 4 or x.dtype != torch.float32:
+        raise ValueError("node features must be (N, C, H, W) float32")
+    _require_device(x)
+    if m == _lib.MODE_COPY_MEAN:
+        gb = None
+    elif logits:
+        m |= _lib.GB_LOGITS
+    return FilmMeanCatFunction.apply(x, gb, csr, m)

@@ -22,27 +22,37 @@ namespace mrp_enc {
 
 constexpr int NIN = 9;  // relative pose width (dgl/utils.py:77)
 
-// One thread per (edge, 4 consecutive hidden units): the edge's 9 pose values are a broadcast
-// load shared by the C/4 threads of the edge; W1 rows are L1/L2-resident.
+constexpr int EPB = 4;  // edges per workgroup
+
+// Workgroup = EPB edges x all C hidden units; thread -> hidden units k = tid, tid + 256, ... whose W1
+// rows and b1 it keeps in registers across the EPB edges.  Edge pose values are wave-uniform
+// (scalar loads); each store instruction writes 256 contiguous bytes of h.
+template <int KPT>
 __global__ void __launch_bounds__(256) edge_hidden_fwd(const float* __restrict__ pose, const float* __restrict__ w1,
                                                        const float* __restrict__ b1, float* __restrict__ h, int E,
                                                        int C) {
-  const int64_t cq = ((int64_t)C + 3) / 4;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)E * cq) return;
-  const int64_t e = idx / cq;
-  const int k0 = (int)(idx - e * cq) * 4;
-  float p[NIN];
+  float w[KPT][NIN + 1];
 #pragma unroll
-  for (int i = 0; i < NIN; ++i) p[i] = pose[e * NIN + i];
+  for (int j = 0; j < KPT; ++j) {
+    const int k = threadIdx.x + 256 * j;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int k = k0 + q;
-    if (k >= C) break;
-    float acc = b1[k];
+    for (int i = 0; i < NIN; ++i) w[j][i] = k < C ? w1[(int64_t)k * NIN + i] : 0.f;
+    w[j][NIN] = k < C ? b1[k] : 0.f;
+  }
+  const int e_end = min(E, (int)(blockIdx.x + 1) * EPB);
+  for (int e = blockIdx.x * EPB; e < e_end; ++e) {
+    float p[NIN];
 #pragma unroll
-    for (int i = 0; i < NIN; ++i) acc = fmaf(p[i], w1[(int64_t)k * NIN + i], acc);
-    h[e * C + k] = acc > 0.f ? acc : 0.f;
+    for (int i = 0; i < NIN; ++i) p[i] = pose[(int64_t)e * NIN + i];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const int k = threadIdx.x + 256 * j;
+      if (k >= C) break;
+      float acc = w[j][NIN];
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) acc = fmaf(p[i], w[j][i], acc);
+      h[(int64_t)e * C + k] = acc > 0.f ? acc : 0.f;
+    }
   }
 }
 
@@ -53,10 +63,18 @@ extern "C" int mrp_edge_hidden_fwd(const float* pose, const float* w1, const flo
   if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
   if (num_edges == 0 || C == 0) return hipSuccess;
   if (!pose || !w1 || !b1 || !h) return hipErrorInvalidValue;
-  const int64_t threads = (int64_t)num_edges * ((C + 3) / 4);
-  const int64_t blocks = (threads + 255) / 256;
+  const int64_t blocks = ((int64_t)num_edges + mrp_enc::EPB - 1) / mrp_enc::EPB;
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(mrp_enc::edge_hidden_fwd, dim3((unsigned)blocks), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), pose, w1, b1, h, num_edges, C);
+  const int kpt = (C + 255) / 256;  // hidden units per thread
+  hipStream_t st = static_cast<hipStream_t>(stream);
+#define MRP_HIDDEN(KPT) \
+  hipLaunchKernelGGL(mrp_enc::edge_hidden_fwd<KPT>, dim3((unsigned)blocks), dim3(256), 0, st, pose, w1, b1, h, num_edges, C)
+  if (kpt <= 1) MRP_HIDDEN(1);
+  else if (kpt <= 2) MRP_HIDDEN(2);
+  else if (kpt <= 4) MRP_HIDDEN(4);
+  else if (kpt <= 8) MRP_HIDDEN(8);
+  else if (kpt <= 16) MRP_HIDDEN(16);
+  else return hipErrorInvalidValue;  // C > 4096
+#undef MRP_HIDDEN
   return hipGetLastError();
 }

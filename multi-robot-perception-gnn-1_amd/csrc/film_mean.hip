@@ -56,6 +56,8 @@ struct AggArgs {
   float* out;  // fwd: out, bwd: grad_x
   int64_t os;
   float* dgb;  // bwd: grad of gb (E, C, 2)
+  const float* dxb;  // bwd: optional grad_x base (added to grad_x), node stride dxbs
+  int64_t dxbs;
   int32_t C, P, PV, mode;
   int32_t lpc;  // lanes per channel plane (power of two <= 64)
   int32_t cpb;  // channels per workgroup
@@ -451,8 +453,12 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
     for (int u = 0; u < NT; ++u) {
       if (!COMPLETE && u >= n) break;
       Frag<VEC> acc;
+      if (a.dxb) {
+        acc = load_frag<VEC, true>(a.dxb + (int64_t)(node0 + u) * a.dxbs + (int64_t)c * a.P + off);
+      } else {
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
+        for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
+      }
 #pragma unroll
       for (int v4 = 0; v4 < NTP; v4 += 4) {
         const f4 w = *reinterpret_cast<const f4*>(W + u * NTP + v4);
@@ -561,8 +567,12 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
           for (int u = 0; u < NT; ++u) {
             if (!COMPLETE && u >= n) break;
             Frag<VEC> acc;
+            if (a.dxb) {
+              acc = load_frag<VEC, true>(a.dxb + (int64_t)(node0 + u) * a.dxbs + (int64_t)c * a.P + off);
+            } else {
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
+              for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
+            }
 #pragma unroll
             for (int v4 = 0; v4 < NTP; v4 += 4) {
               const f4 w = *reinterpret_cast<const f4*>(W + u * NTP + v4);
@@ -815,7 +825,7 @@ bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* ei
 
 extern "C" {
 
-int mrp_abi_version(void) { return 4; }
+int mrp_abi_version(void) { return 5; }
 
 const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
 
@@ -863,7 +873,8 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
                       const float* gb, const int32_t* indptr, const int32_t* src, const int32_t* eid,
                       const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
                       int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode_flags, float* grad_x,
-                      int64_t gx_node_stride, float* grad_gb, void* stream) {
+                      int64_t gx_node_stride, const float* grad_x_base, int64_t base_node_stride, float* grad_gb,
+                      void* stream) {
   const int32_t logits = (mode_flags & MRP_AGG_GB_LOGITS) ? 1 : 0;
   const int32_t mode = mode_flags & ~MRP_AGG_GB_LOGITS;
   if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind, num_nodes, num_edges, C, P,
@@ -883,10 +894,12 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   const int64_t plane = (int64_t)C * P;
   if (grad_out == nullptr || g_node_stride < plane) return hipErrorInvalidValue;
   if (want_dx && gx_node_stride < plane) return hipErrorInvalidValue;
+  if (want_dx && grad_x_base != nullptr && base_node_stride < plane) return hipErrorInvalidValue;
   if (want_dgb && (x == nullptr || x_node_stride < plane)) return hipErrorInvalidValue;
   if (!copy && num_edges > 0 && gb == nullptr) return hipErrorInvalidValue;
   bool vec4 = (P % 4 == 0) && (g_node_stride % 4 == 0) && aligned16(grad_out);
   if (want_dx) vec4 = vec4 && (gx_node_stride % 4 == 0) && aligned16(grad_x);
+  if (want_dx && grad_x_base) vec4 = vec4 && (base_node_stride % 4 == 0) && aligned16(grad_x_base);
   if (want_dgb) vec4 = vec4 && (x_node_stride % 4 == 0) && aligned16(x);
   // With the Gram accumulators live (N >= 5 and d gamma/beta wanted), 16-byte slices cost
   // occupancy (234 VGPRs at N=8); 8-byte slices keep 3 waves/SIMD and stream faster.
@@ -918,6 +931,8 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   a.want_dx = want_dx ? 1 : 0;
   a.want_dgb = want_dgb ? 1 : 0;
   a.logits = logits;
+  a.dxb = want_dx ? grad_x_base : nullptr;
+  a.dxbs = base_node_stride;
   return dispatch_bwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, st);
 }
 

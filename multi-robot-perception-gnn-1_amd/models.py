@@ -27,7 +27,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from .aggregate import film_mean
+from .aggregate import film_mean, film_mean_cat
 from .encoder import edge_logits
 
 
@@ -87,6 +87,18 @@ class GCN(nn.Module):
         z = self.edge_encoder.logits(g.edata["pose"])
         return film_mean(x, z, g.csr(x.device), mode, logits=True)
 
+    def forward_cat(self, g, feats: torch.Tensor = None) -> torch.Tensor:
+        """``torch.cat((feats, self(g, feats)), 1)`` (``models.py:181-182``) with the aggregate written
+        straight into the concatenation buffer (and the backward fused likewise)."""
+        x = g.ndata["image"] if feats is None else feats
+        if _opt(self.opt, "gcn_return", "aggregate") == "input" or not x.is_cuda:
+            return torch.cat((x, self(g, x)), dim=1)
+        mode = _opt(self.opt, "gcn_mode", "film_mean")
+        if mode == "copy_mean":
+            return film_mean_cat(x, None, g.csr(x.device), mode)
+        z = self.edge_encoder.logits(g.edata["pose"])
+        return film_mean_cat(x, z, g.csr(x.device), mode, logits=True)
+
 
 class GCNBlock(nn.Module):
     """GCN stacking of ``multi_view_dgl_model`` (``dgl/model/models.py:162-171,180-189``)."""
@@ -103,14 +115,11 @@ class GCNBlock(nn.Module):
             self.conv2 = nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1)
 
     def forward(self, g, h: torch.Tensor) -> torch.Tensor:
-        g_h = self.gcn1(g, h)
-        h = torch.cat((h, g_h), dim=1)
+        h = self.gcn1.forward_cat(g, h)  # cat((h, gcn1(h)), 1)
         if self.opt.compress_gcn:
             h = self.conv1(h)
         if self.opt.multi_gcn:
-            g_h = self.gcn2(g, h)
-            h = torch.cat((h, g_h), dim=1)
-            h = self.conv2(h)
+            h = self.conv2(self.gcn2.forward_cat(g, h))
         return h
 
 
@@ -151,15 +160,12 @@ class multi_view_dgl_model(nn.Module):  # noqa: N801  (reference class name)
         with g.local_scope():
             h = self.features(g)
             g.ndata["image"] = h
-            g_h = self.gcn1(g)
-            h = torch.cat((h, g_h), dim=1)
+            h = self.gcn1.forward_cat(g)  # cat((h, gcn1(g)), 1), models.py:181-182
             if self.opt.compress_gcn:
                 h = self.conv1(h)
             if self.opt.multi_gcn:
                 g.ndata["image"] = h
-                g_h = self.gcn2(g)
-                h = torch.cat((h, g_h), dim=1)
-                h = self.conv2(h)
+                h = self.conv2(self.gcn2.forward_cat(g))  # models.py:186-189
             if not hasattr(self, "decoder"):
                 return h
             return self.decoder(h)

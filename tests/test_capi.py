@@ -77,7 +77,7 @@ def test_argument_validation_without_launch():
     assert _fwd(lib, kind=1, B=2, maxn=4, Nt=8, E=24, C=0, P=16) == 0  # consistent, empty features: no-op
     # bwd: nothing requested -> no-op
     assert lib.mrp_film_mean_bwd(None, 0, None, 0, None, None, None, None, None, 0, 0, 0, 0, 0, 0, 0, 0, None, 0,
-                                 None, None) == 0
+                                 None, 0, None, None) == 0
 
 
 def test_no_cpu_fallback():

@@ -327,3 +327,23 @@ def test_complete_fast_path_equals_csr_path(cuda_device, n, hw):
     assert torch.equal(res[0][0], res[1][0])
     assert rel_err(res[0][1].numpy(), res[1][1].numpy()) <= 1e-6
     assert rel_err(res[0][2].numpy(), res[1][2].numpy()) <= 1e-6
+
+
+@pytest.mark.parametrize("complete", [True, False])
+def test_cat_fused_forward_backward(cuda_device, complete):
+    """film_mean_cat == torch.cat((x, film_mean(x)), 1), forward exactly, backward (incl. the
+    grad_x_base accumulation of the concatenation's first half) to rounding."""
+    g, x, gb = random_case(8, 16, 8, 8, seed=31, bnn=[8, 8, 8])
+    csr = g.csr(cuda_device, allow_complete=complete)
+    x1 = x.to(cuda_device).requires_grad_(True)
+    x2 = x.to(cuda_device).requires_grad_(True)
+    z1 = gb.to(cuda_device).requires_grad_(True)
+    z2 = gb.to(cuda_device).requires_grad_(True)
+    a = m.film_mean_cat(x1, z1, csr, logits=True)
+    b = torch.cat((x2, m.film_mean(x2, z2, csr, logits=True)), 1)
+    assert torch.equal(a, b)
+    G = torch.randn_like(a)
+    a.backward(G)
+    b.backward(G)
+    assert rel_err(x1.grad.cpu().numpy(), x2.grad.cpu().numpy()) <= 1e-6
+    assert rel_err(z1.grad.cpu().numpy(), z2.grad.cpu().numpy()) <= 1e-6
