@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
 // Backward, grad_x only (used for NT > 8, where the fused kernel's Gram accumulators would not
 // fit in registers):  grad_x[u] = sum_v Wt[u][v] * G[v].
 // ---------------------------------------------------------------------------
-template <int NT, int VEC, bool COMPLETE>
+template <int NT, int VEC, bool COMPLETE, bool DXB>
 __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
@@ -453,7 +453,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
     for (int u = 0; u < NT; ++u) {
       if (!COMPLETE && u >= n) break;
       Frag<VEC> acc;
-      if (a.dxb) {
+      if (DXB) {  // grad_x_base: a separate instantiation (it costs registers)
         acc = load_frag<VEC, true>(a.dxb + (int64_t)(node0 + u) * a.dxbs + (int64_t)c * a.P + off);
       } else {
 #pragma unroll
@@ -476,12 +476,23 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
   }
 }
 
-// Reduce a value over the lpc lanes of one channel group (lpc is a power of two <= 64).  The six
-// butterfly steps are unrolled; the ones wider than the group are skipped by a uniform branch.
+// Cross-lane move with a DPP control (no LDS traffic).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, true));
+}
+
+// Reduce a value over the lpc lanes of one channel group (lpc is a power of two <= 64); every lane
+// of the group ends with the sum.  Butterfly: xor 1 and xor 2 by quad_perm, 4 <-> 4 by
+// row_half_mirror, 8 <-> 8 by row_mirror (all DPP modifiers on the add), then xor 16 / xor 32 by
+// ds_bpermute.  Steps wider than the group are skipped by a uniform branch.
 __device__ __forceinline__ float group_sum(float x, int lpc) {
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1)
-    if (m < lpc) x += __shfl_xor(x, m, 64);
+  if (lpc >= 2) x += dpp_mov<0xB1>(x);   // quad_perm [1,0,3,2]
+  if (lpc >= 4) x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]
+  if (lpc >= 8) x += dpp_mov<0x141>(x);  // row_half_mirror
+  if (lpc >= 16) x += dpp_mov<0x140>(x);  // row_mirror
+  if (lpc >= 32) x += __shfl_xor(x, 16, 64);
+  if (lpc >= 64) x += __shfl_xor(x, 32, 64);
   return x;
 }
 
@@ -492,7 +503,7 @@ __device__ __forceinline__ float group_sum(float x, int lpc) {
 //   grad_gb[e, c] = (s_v * D[v][u], s_v * S[v])    for every edge e = (u -> v).
 // For NT > 8 the kernel runs with VB = 4 and loops over destination blocks (x re-read from L2).
 // ---------------------------------------------------------------------------
-template <int NT, int VB, int VEC, bool COMPLETE, int MINW = 1>
+template <int NT, int VB, int VEC, bool COMPLETE, bool DXB = false, int MINW = 1>
 __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
@@ -567,7 +578,7 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
           for (int u = 0; u < NT; ++u) {
             if (!COMPLETE && u >= n) break;
             Frag<VEC> acc;
-            if (a.dxb) {
+            if (DXB) {  // grad_x_base: a separate instantiation (it costs registers)
               acc = load_frag<VEC, true>(a.dxb + (int64_t)(node0 + u) * a.dxbs + (int64_t)c * a.P + off);
             } else {
 #pragma unroll
@@ -732,28 +743,28 @@ hipError_t launch_fwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int NT, bool COMPLETE>
-hipError_t launch_bwd_nt(const AggArgs& a_in, const Geometry& g, hipStream_t st) {
+template <int NT, bool COMPLETE, bool DXB>
+hipError_t launch_bwd_ntb(const AggArgs& a_in, const Geometry& g, hipStream_t st) {
   if constexpr (NT <= 8) {
     const AggArgs& a = a_in;
     const size_t lds = lds_bwd<NT>(g.cpb);
     if (g.vec == 4)
-      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 4, COMPLETE>), lds);
+      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 4, COMPLETE, DXB>), lds);
     else if (g.vec == 2)
-      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 2, COMPLETE>), lds);
+      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 2, COMPLETE, DXB>), lds);
     else
-      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 1, COMPLETE>), lds);
+      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 1, COMPLETE, DXB>), lds);
     return hipGetLastError();
   } else {
     if (a_in.want_dx) {
       const AggArgs& a = a_in;
       const size_t lds = lds_dx<NT>(g.cpb);
       if (g.vec == 4)
-        MRP_LAUNCH((mrp::film_bwd_dx<NT, 4, COMPLETE>), lds);
+        MRP_LAUNCH((mrp::film_bwd_dx<NT, 4, COMPLETE, DXB>), lds);
       else if (g.vec == 2)
-        MRP_LAUNCH((mrp::film_bwd_dx<NT, 2, COMPLETE>), lds);
+        MRP_LAUNCH((mrp::film_bwd_dx<NT, 2, COMPLETE, DXB>), lds);
       else
-        MRP_LAUNCH((mrp::film_bwd_dx<NT, 1, COMPLETE>), lds);
+        MRP_LAUNCH((mrp::film_bwd_dx<NT, 1, COMPLETE, DXB>), lds);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
@@ -771,6 +782,11 @@ hipError_t launch_bwd_nt(const AggArgs& a_in, const Geometry& g, hipStream_t st)
     }
     return hipSuccess;
   }
+}
+
+template <int NT, bool COMPLETE>
+hipError_t launch_bwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  return a.dxb ? launch_bwd_ntb<NT, COMPLETE, true>(a, g, st) : launch_bwd_ntb<NT, COMPLETE, false>(a, g, st);
 }
 
 #define MRP_DISPATCH_NT(NTV, COMPLETE, FN, ...)                                        \
@@ -901,10 +917,9 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   if (want_dx) vec4 = vec4 && (gx_node_stride % 4 == 0) && aligned16(grad_x);
   if (want_dx && grad_x_base) vec4 = vec4 && (base_node_stride % 4 == 0) && aligned16(grad_x_base);
   if (want_dgb) vec4 = vec4 && (x_node_stride % 4 == 0) && aligned16(x);
-  // With the Gram accumulators live (N >= 5 and d gamma/beta wanted), 16-byte slices cost
-  // occupancy (234 VGPRs at N=8); 8-byte slices keep 3 waves/SIMD and stream faster.
-  // (Measured on the complete-graph kernels; the CSR kernels keep 16-byte slices.)
-  const int vec = vec4 ? ((want_dgb && max_nodes >= 5 && graph_kind == MRP_GRAPH_COMPLETE) ? 2 : 4) : 1;
+  // 16-byte slices: with the DPP lane reduction they beat 8-byte slices (310 vs 322 us at B=32,
+  // N=8, C=512, 32x32) despite 2 waves/SIMD instead of 3.  VEC=2 stays compiled for experiments.
+  const int vec = vec4 ? 4 : 1;
   Geometry g = make_geometry(C, P, vec);
   g.grid = (int64_t)num_graphs * g.ncb;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;

@@ -7,7 +7,7 @@
 //   film_fwd<N,4> : the product kernel at several (lanes-per-channel, channels-per-block) geometries
 // Usage: kernel_lab [B N C HW iters]
 #include "../multi-robot-perception-gnn-1_amd/csrc/film_mean.hip"
-#include "../multi-robot-perception-gnn-1_amd/csrc/edge_encoder.hip"
+
 
 #include <algorithm>
 #include <cstdio>
@@ -149,21 +149,30 @@ int main(int argc, char** argv) {
   const int C = argc > 3 ? atoi(argv[3]) : 512;
   const int HW = argc > 4 ? atoi(argv[4]) : 32;
   const int iters = argc > 5 ? atoi(argv[5]) : 30;
+  const int KNN = argc > 6 ? atoi(argv[6]) : 0;  // 0: complete graphs; k: k in-edges per node (CSR path)
   const int P = HW * HW;
   const int Nt = B * N;
-  const int E = B * N * (N - 1);
+  const int E = KNN ? B * N * KNN : B * N * (N - 1);
   std::vector<int> indptr(Nt + 1), src(E), eid(E), goff(B + 1);
-  // complete i-major graphs, CSR by destination
   int k = 0;
   for (int b = 0; b < B; ++b) {
     goff[b] = b * N;
     for (int v = 0; v < N; ++v) {
       indptr[b * N + v] = k;
-      for (int u = 0; u < N; ++u) {
-        if (u == v) continue;
-        src[k] = b * N + u;
-        eid[k] = b * N * (N - 1) + u * (N - 1) + (v < u ? v : v - 1);
-        ++k;
+      if (KNN) {
+        // k sources per destination, ascending local ids (a k-NN-shaped graph), edge ids = CSR order
+        std::vector<int> us;
+        for (int i = 1; i <= KNN; ++i) us.push_back((v + i) % N);
+        std::sort(us.begin(), us.end());
+        for (int u : us) { src[k] = b * N + u; eid[k] = k; ++k; }
+      } else {
+        // complete i-major graphs, CSR by destination
+        for (int u = 0; u < N; ++u) {
+          if (u == v) continue;
+          src[k] = b * N + u;
+          eid[k] = b * N * (N - 1) + u * (N - 1) + (v < u ? v : v - 1);
+          ++k;
+        }
       }
     }
   }
@@ -195,7 +204,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(gb, hg.data(), hg.size() * 4, hipMemcpyHostToDevice));
   }
   const double alg = (double)feat * 8 + (double)E * C * 2 * 4;
-  printf("workload B=%d N=%d C=%d %dx%d: alg bytes %.1f MB\n", B, N, C, HW, HW, alg / 1e6);
+  printf("workload B=%d N=%d C=%d %dx%d %s: alg bytes %.1f MB\n", B, N, C, HW, HW, KNN ? "knn" : "complete",
+         alg / 1e6);
   auto report = [&](const char* name, float ms, double bytes) {
     printf("%-40s %9.1f us  %7.0f GB/s  %5.1f%% of 8 TB/s\n", name, ms * 1e3, bytes / ms / 1e6,
            bytes / ms / 1e6 / 80.0);
@@ -217,7 +227,7 @@ int main(int argc, char** argv) {
     a.ncb = (C + cpb - 1) / cpb;
     return a;
   };
-  if (N == 8) {
+  if (N == 8 && !KNN) {
     for (int lpc : {64, 32, 16}) {
       for (int cpb : {4, 8, 16}) {
         if (lpc * cpb > 256 || lpc * cpb < 64) continue;
@@ -235,7 +245,7 @@ int main(int argc, char** argv) {
     }
   }
 
-  if (N == 8) {
+  if (N == 8 && !KNN) {
     mrp::AggArgs a = args_for(64, 4);
     const int items = B * a.ncb;
     const size_t lds = (size_t)(2 * 4 * mrp::Tile<8>::SZ + 2 * mrp::Tile<8>::NTP) * 4;
@@ -261,7 +271,7 @@ int main(int argc, char** argv) {
     VAR(false, false, true, true, 1024)
     VAR(false, true, false, true, 1024)
   }
-  if (N == 8) {
+  if (N == 8 && !KNN) {
     // backward variants: slice width (VEC) and waves/SIMD bound
     float* dgb;
     CK(hipMalloc(&dgb, (size_t)E * C * 2 * 4));
@@ -271,14 +281,14 @@ int main(int argc, char** argv) {
       a.x = x; a.xs = (int64_t)C * P; a.g = gout; a.gs = (int64_t)C * P; a.gb = gb; a.goff = d_goff;
       a.indptr = d_indptr; a.src = d_src; a.eid = d_eid; a.out = out; a.os = (int64_t)C * P; a.dgb = dgb;
       a.C = C; a.P = P; a.PV = P / vec; a.mode = 0; a.lpc = 64; a.cpb = 4; a.ncb = C / 4;
-      a.want_dx = 1; a.want_dgb = 1;
+      a.want_dx = 1; a.want_dgb = 1; a.logits = 1;
       return a;
     };
     const size_t lds = (size_t)(2 * 4 * mrp::Tile<8>::SZ + 4 * mrp::Tile<8>::NTP + mrp::Tile<8>::NTP) * 4;
 #define BVAR(VEC, MINW)                                                                                  \
     {                                                                                                    \
       mrp::AggArgs a = bargs(VEC);                                                                       \
-      float ms_ = time_ms([&] { hipLaunchKernelGGL((mrp::film_bwd_fused<8, 8, VEC, true, MINW>),         \
+      float ms_ = time_ms([&] { hipLaunchKernelGGL((mrp::film_bwd_fused<8, 8, VEC, true, false, MINW>),         \
                                                    dim3(B * a.ncb), dim3(256), lds, 0, a); }, iters);    \
       char nm_[96];                                                                                      \
       snprintf(nm_, sizeof nm_, "bwd_fused<8> vec=%d minw=%d", VEC, MINW);                              \
@@ -292,7 +302,10 @@ int main(int argc, char** argv) {
     CK(hipFree(dgb));
   }
   // product entry points (default geometry), both graph kinds
+  float* dgb_prod;
+  CK(hipMalloc(&dgb_prod, (size_t)E * C * 2 * 4));
   for (int kind : {MRP_GRAPH_CSR, MRP_GRAPH_COMPLETE}) {
+    if (KNN && kind == MRP_GRAPH_COMPLETE) continue;
     char nm[96];
     float ms = time_ms([&] {
       CK((hipError_t)mrp_film_mean_fwd(x, (int64_t)C * P, gb, d_indptr, d_src, d_eid, d_goff, B, N, kind, Nt, E, C,
@@ -302,37 +315,12 @@ int main(int argc, char** argv) {
     report(nm, ms, alg);
     ms = time_ms([&] {
       CK((hipError_t)mrp_film_mean_bwd(gout, (int64_t)C * P, x, (int64_t)C * P, gb, d_indptr, d_src, d_eid, d_goff, B,
-                                       N, kind, Nt, E, C, P, 0, out, (int64_t)C * P, gb, nullptr));
+                                       N, kind, Nt, E, C, P, MRP_AGG_GB_LOGITS, out, (int64_t)C * P, nullptr, 0,
+                                       dgb_prod, nullptr));
     }, iters);
     snprintf(nm, sizeof nm, "mrp_film_mean_bwd kind=%s (dx+dgb)", kind ? "complete" : "csr");
     // bwd alg bytes: read G and x, write dx, read gb, write dgb
     report(nm, ms, (double)feat * 12 + (double)E * C * 2 * 8);
-  }
-  {
-    // fused edge encoder on the same E edges (C -> 2C)
-    float *pose, *w1, *b1, *w2, *b2, *eo;
-    CK(hipMalloc(&pose, (size_t)E * 9 * 4));
-    CK(hipMalloc(&w1, (size_t)C * 9 * 4));
-    CK(hipMalloc(&b1, (size_t)C * 4));
-    CK(hipMalloc(&w2, (size_t)2 * C * C * 4));
-    CK(hipMalloc(&b2, (size_t)2 * C * 4));
-    CK(hipMalloc(&eo, (size_t)E * 2 * C * 4));
-    auto fill = [](float* d, size_t n, float scale) {  // random data: MFMA clocks differ on zeros
-      std::vector<float> h(n);
-      uint32_t s = 12345u;
-      for (auto& v : h) { s = s * 1664525u + 1013904223u; v = scale * ((float)(s >> 8) / 16777216.f - 0.5f); }
-      CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
-    };
-    fill(pose, (size_t)E * 9, 10.f);
-    fill(w1, (size_t)C * 9, 0.6f);
-    fill(b1, (size_t)C, 0.6f);
-    fill(w2, (size_t)2 * C * C, 0.08f);
-    fill(b2, (size_t)2 * C, 0.08f);
-    float ms = time_ms([&] { CK((hipError_t)mrp_edge_encoder_fwd(pose, w1, b1, w2, b2, E, C, eo, nullptr)); }, iters);
-    const double flops = 2.0 * E * (9.0 * C + 2.0 * C * C);
-    printf("%-40s %9.1f us  %7.1f TFLOP/s  %5.1f%% of 157 TF fp32\n", "mrp_edge_encoder_fwd", ms * 1e3,
-           flops / ms / 1e9, flops / ms / 1e9 / 157.3 * 100);
-    CK(hipFree(pose)); CK(hipFree(w1)); CK(hipFree(b1)); CK(hipFree(w2)); CK(hipFree(b2)); CK(hipFree(eo));
   }
   CK(hipFree(x));
   CK(hipFree(out));
