@@ -55,6 +55,12 @@ enum mrp_graph_kind {
     MRP_GRAPH_CSR = 0,
     MRP_GRAPH_COMPLETE = 1
 };
+/* MRP_GRAPH_REGULAR(k): a CSR graph in which every node has exactly k in-edges (k-NN graphs).  The
+ * CSR arrays are read as for MRP_GRAPH_CSR; the backward for graphs of more than 8 nodes then keeps
+ * one Gram accumulator per edge instead of per node pair (k <= 8).  num_edges must be k*num_nodes. */
+#define MRP_GRAPH_REGULAR(k) (((k) << 8) | 2)
+#define MRP_GRAPH_IS_REGULAR(kind) (((kind) & 0xff) == 2)
+#define MRP_GRAPH_REGULAR_K(kind) ((kind) >> 8)
 
 /* Aggregation modes (the reference's UDF variants). */
 enum mrp_agg_mode {
@@ -81,7 +87,7 @@ enum mrp_agg_mode {
  *   src, eid   (num_edges) int32
  *   graph_off  (num_graphs + 1) int32 node offsets of the batched graphs
  *   max_nodes  max_b (graph_off[b+1] - graph_off[b]), 0..MRP_MAX_NODES (host-known)
- *   graph_kind MRP_GRAPH_CSR or MRP_GRAPH_COMPLETE (see enum mrp_graph_kind)
+ *   graph_kind MRP_GRAPH_CSR, MRP_GRAPH_COMPLETE or MRP_GRAPH_REGULAR(k) (see enum mrp_graph_kind)
  *   out        (num_nodes, C, P) fp32, node stride out_node_stride (elements)
  */
 int mrp_film_mean_fwd(const float* x, int64_t x_node_stride,

@@ -25,7 +25,7 @@ EXPORTED_SYMBOLS = (
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_NODES = 16
 
 MODE_FILM_MEAN = 0
@@ -34,6 +34,14 @@ MODE_COPY_MEAN = 2
 GB_LOGITS = 0x100  # mode flag: gb holds pre-sigmoid logits
 GRAPH_CSR = 0
 GRAPH_COMPLETE = 1
+
+
+MAX_REGULAR_K = 8  # largest in-degree the per-edge-slot backward handles
+
+
+def graph_regular(k: int) -> int:
+    """MRP_GRAPH_REGULAR(k): every node has exactly k in-edges."""
+    return (k << 8) | 2
 MODES = {"film_mean": MODE_FILM_MEAN, "film_sum": MODE_FILM_SUM, "copy_mean": MODE_COPY_MEAN}
 
 _lock = threading.Lock()

@@ -64,6 +64,7 @@ struct AggArgs {
   int32_t ncb;  // channel blocks per graph
   int32_t want_dx, want_dgb;
   int32_t logits;  // gb holds pre-sigmoid logits (MRP_AGG_GB_LOGITS): apply sigmoid on load
+  int32_t kdeg;    // MRP_GRAPH_REGULAR: every node's in-degree (else 0)
 };
 
 __device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
@@ -685,6 +686,163 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Backward for REGULAR graphs (every node has exactly K = a.kdeg in-edges, e.g. k-NN), N > 8:
+// one sweep like film_bwd_fused, but the Gram is kept per edge slot, D[v][j] = sum_p G_v x_{u(v,j)},
+// N*KMAX accumulators instead of N*N.  The source u(v,j) is wave-uniform (the graph is shared by the
+// workgroup), so x_{u} is a uniform dynamic index into the register array (s_set_gpr_idx), not a
+// scratch access.  grad_x uses the dense transposed tiles.  Multi-edges and self-loops are just
+// slots.  Deterministic like the other kernels.
+// ---------------------------------------------------------------------------
+template <int NT, int KMAX, int VEC, bool DXB>
+__global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
+  constexpr int SZ = Tile<NT>::SZ;
+  constexpr int NTP = Tile<NT>::NTP;
+  constexpr int NS = NT * KMAX;  // edge slots
+  extern __shared__ float4 smem_f4[];
+  float* smem = reinterpret_cast<float*>(smem_f4);
+  float* Wt = smem;                          // [cpb][NT][NTP] scaled, transposed
+  float* Dl = Wt + a.cpb * SZ;               // [cpb][NS]
+  float* Sl = Dl + a.cpb * NS;               // [cpb][NTP]
+  float* sc = Sl + a.cpb * NTP;              // [NTP]
+  int* slot_u = reinterpret_cast<int*>(sc + NTP);  // [NS] local source of slot (v, j)
+  int* slot_e = slot_u + NS;                       // [NS] edge id of slot (v, j)
+
+  const int b = blockIdx.x / a.ncb;
+  const int cb = blockIdx.x - b * a.ncb;
+  const int node0 = a.goff[b];
+  const int n = min(a.goff[b + 1] - node0, NT);
+  if (n <= 0) return;
+  const int c0 = cb * a.cpb;
+  const int K = a.kdeg;
+
+  for (int t = threadIdx.x; t < NS; t += blockDim.x) {
+    const int v = t / KMAX, j = t - v * KMAX;
+    int u = 0, e = -1;
+    const int k = v < n ? a.indptr[node0 + v] + j : 0;
+    if (v < n && j < K && k < a.indptr[node0 + v + 1]) {  // the host checked the degrees; stay in bounds anyway
+      u = a.src[k] - node0;
+      e = a.eid[k];
+      if ((unsigned)u >= (unsigned)n) { u = 0; e = -1; }  // leaves the graph: rejected on the host
+    }
+    slot_u[t] = u;
+    slot_e[t] = e;
+  }
+  build_tiles_csr<NT, true>(a, node0, n, c0, Wt, nullptr, sc, nullptr);
+  __syncthreads();
+
+  const int grp = threadIdx.x / a.lpc;
+  const int li = threadIdx.x - grp * a.lpc;
+  const int c = c0 + grp;
+  const bool active = grp < a.cpb && c < a.C;
+  const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c * a.P;
+  const float* xbase = a.x + (int64_t)node0 * a.xs + (int64_t)c * a.P;
+  float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
+
+  float D[NS];
+  float S[NT];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) D[i] = 0.f;
+#pragma unroll
+  for (int v = 0; v < NT; ++v) S[v] = 0.f;
+
+  if (active) {
+    for (int j = li; j < a.PV; j += a.lpc) {
+      const int64_t off = (int64_t)j * VEC;
+      int tile = grp * SZ;  // laundered: keep the weights in LDS, not hoisted into registers
+      asm volatile("" : "+v"(tile));
+      const float* W = Wt + tile;
+      float gv[NT][VEC];
+      float xv[NT][VEC];
+#pragma unroll
+      for (int v = 0; v < NT; ++v) {
+        const int vv = v < n ? v : n - 1;
+        const Frag<VEC> f = load_frag<VEC, true>(gbase + (int64_t)vv * a.gs + off);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) gv[v][k] = f.v[k];
+      }
+      if (a.want_dgb) {
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          const int uu = u < n ? u : n - 1;
+          const Frag<VEC> f = load_frag<VEC, true>(xbase + (int64_t)uu * a.xs + off);
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) xv[u][k] = f.v[k];
+        }
+      }
+      if (a.want_dx) {
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          if (u >= n) break;
+          Frag<VEC> acc;
+          if (DXB) {
+            acc = load_frag<VEC, true>(a.dxb + (int64_t)(node0 + u) * a.dxbs + (int64_t)c * a.P + off);
+          } else {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
+          }
+#pragma unroll
+          for (int v4 = 0; v4 < NTP; v4 += 4) {
+            const f4 w = *reinterpret_cast<const f4*>(W + u * NTP + v4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int v = v4 + q;
+              if (v >= NT) break;
+#pragma unroll
+              for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(w[q], gv[v][k], acc.v[k]);
+            }
+          }
+          store_frag<VEC, true>(ob + (int64_t)u * a.os + off, acc);
+        }
+      }
+      if (a.want_dgb) {
+#pragma unroll
+        for (int v = 0; v < NT; ++v) {
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) S[v] += gv[v][k];
+#pragma unroll
+          for (int jj = 0; jj < KMAX; ++jj) {
+            if (jj >= K) break;
+            const int u = __builtin_amdgcn_readfirstlane(slot_u[v * KMAX + jj]);  // wave-uniform
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) D[v * KMAX + jj] = fmaf(gv[v][k], xv[u][k], D[v * KMAX + jj]);
+          }
+        }
+      }
+    }
+  }
+  if (!a.want_dgb) return;
+#pragma unroll
+  for (int v = 0; v < NT; ++v) {
+    S[v] = group_sum(S[v], a.lpc);
+#pragma unroll
+    for (int jj = 0; jj < KMAX; ++jj) D[v * KMAX + jj] = group_sum(D[v * KMAX + jj], a.lpc);
+  }
+  if (active && li == 0) {
+#pragma unroll
+    for (int v = 0; v < NT; ++v) {
+      Sl[grp * NTP + v] = S[v];
+#pragma unroll
+      for (int jj = 0; jj < KMAX; ++jj) Dl[grp * NS + v * KMAX + jj] = D[v * KMAX + jj];
+    }
+  }
+  __syncthreads();
+  // per-edge outputs: thread -> (channel fastest, slot)
+  for (int t = threadIdx.x; t < a.cpb * NS; t += blockDim.x) {
+    const int cl = t % a.cpb;
+    const int slot = t / a.cpb;
+    const int v = slot / KMAX;
+    const int cc = c0 + cl;
+    const int e = slot_e[slot];
+    if (e < 0 || cc >= a.C) continue;
+    const float s = sc[v];
+    const int64_t off = ((int64_t)e * a.C + cc) * 2;
+    float2 r = make_float2(s * Dl[cl * NS + slot], s * Sl[cl * NTP + v]);
+    if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
+    *reinterpret_cast<float2*>(a.dgb + off) = r;
+  }
+}
+
 }  // namespace mrp
 
 // ===========================================================================
@@ -725,6 +883,12 @@ size_t lds_fwd(int cpb) {
 template <int NT>
 size_t lds_dx(int cpb) {
   return (size_t)(cpb * mrp::Tile<NT>::SZ + mrp::Tile<NT>::NTP) * sizeof(float);
+}
+template <int NT, int KMAX>
+size_t lds_regular(int cpb) {
+  return (size_t)(cpb * mrp::Tile<NT>::SZ + cpb * NT * KMAX + cpb * mrp::Tile<NT>::NTP + mrp::Tile<NT>::NTP) *
+             sizeof(float) +
+         2 * (size_t)NT * KMAX * sizeof(int);
 }
 template <int NT>
 size_t lds_bwd(int cpb) {
@@ -784,8 +948,29 @@ hipError_t launch_bwd_ntb(const AggArgs& a_in, const Geometry& g, hipStream_t st
   }
 }
 
+template <int NT, int KMAX, bool DXB>
+hipError_t launch_bwd_regular(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  // VEC 4 would need 4*NT registers more per operand and spills; KMAX 8 only fits at VEC 1
+  const size_t lds = lds_regular<NT, KMAX>(g.cpb);
+  if constexpr (KMAX <= 4) {
+    if (g.vec >= 2) {
+      MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 2, DXB>), lds);
+      return hipGetLastError();
+    }
+  }
+  MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 1, DXB>), lds);
+  return hipGetLastError();
+}
+
 template <int NT, bool COMPLETE>
 hipError_t launch_bwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  if constexpr (NT > 8 && !COMPLETE) {
+    // regular in-degree (k-NN): per-edge-slot Gram, one sweep
+    if (a.kdeg >= 1 && a.kdeg <= 4)
+      return a.dxb ? launch_bwd_regular<NT, 4, true>(a, g, st) : launch_bwd_regular<NT, 4, false>(a, g, st);
+    if (a.kdeg >= 5 && a.kdeg <= 8)
+      return a.dxb ? launch_bwd_regular<NT, 8, true>(a, g, st) : launch_bwd_regular<NT, 8, false>(a, g, st);
+  }
   return a.dxb ? launch_bwd_ntb<NT, COMPLETE, true>(a, g, st) : launch_bwd_ntb<NT, COMPLETE, false>(a, g, st);
 }
 
@@ -829,7 +1014,10 @@ bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* ei
     if ((int64_t)num_graphs * max_nodes * (max_nodes > 0 ? max_nodes - 1 : 0) != num_edges) return false;
     return true;
   }
-  if (graph_kind != MRP_GRAPH_CSR) return false;
+  if (graph_kind != MRP_GRAPH_CSR && !MRP_GRAPH_IS_REGULAR(graph_kind)) return false;
+  if (MRP_GRAPH_IS_REGULAR(graph_kind) && (MRP_GRAPH_REGULAR_K(graph_kind) < 1 ||
+                                          (int64_t)MRP_GRAPH_REGULAR_K(graph_kind) * num_nodes != num_edges))
+    return false;
   if (num_graphs > 0 && graph_off == nullptr) return false;
   if (num_nodes > 0 && indptr == nullptr) return false;
   if (num_edges > 0 && (src == nullptr || eid == nullptr)) return false;
@@ -841,7 +1029,7 @@ bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* ei
 
 extern "C" {
 
-int mrp_abi_version(void) { return 5; }
+int mrp_abi_version(void) { return 6; }
 
 const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
 
@@ -919,7 +1107,9 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   if (want_dgb) vec4 = vec4 && (x_node_stride % 4 == 0) && aligned16(x);
   // 16-byte slices: with the DPP lane reduction they beat 8-byte slices (310 vs 322 us at B=32,
   // N=8, C=512, 32x32) despite 2 waves/SIMD instead of 3.  VEC=2 stays compiled for experiments.
-  const int vec = vec4 ? 4 : 1;
+  int vec = vec4 ? 4 : 1;
+  const int kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
+  if (max_nodes > 8 && kdeg >= 1 && kdeg <= 8) vec = (vec4 && kdeg <= 4) ? 2 : 1;  // film_bwd_regular
   Geometry g = make_geometry(C, P, vec);
   g.grid = (int64_t)num_graphs * g.ncb;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
@@ -948,6 +1138,7 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   a.logits = logits;
   a.dxb = want_dx ? grad_x_base : nullptr;
   a.dxbs = base_node_stride;
+  a.kdeg = kdeg;
   return dispatch_bwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, st);
 }
 

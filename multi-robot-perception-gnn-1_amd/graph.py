@@ -24,7 +24,7 @@ from typing import Dict, Iterable, List, NamedTuple, Optional, Sequence
 import numpy as np
 import torch
 
-from ._lib import GRAPH_COMPLETE, GRAPH_CSR, MAX_NODES
+from ._lib import GRAPH_COMPLETE, GRAPH_CSR, MAX_NODES, MAX_REGULAR_K, graph_regular
 from .pose import relative_pose_batch
 
 
@@ -39,7 +39,7 @@ class GraphCSR(NamedTuple):
     max_nodes: int
     num_nodes: int
     num_edges: int
-    graph_kind: int  # GRAPH_COMPLETE (the reference topology, arithmetic edge ids) or GRAPH_CSR
+    graph_kind: int  # GRAPH_COMPLETE (reference topology, arithmetic edge ids), graph_regular(k) or GRAPH_CSR
 
 
 class _FeatureDict(dict):
@@ -151,6 +151,7 @@ class RobotGraph:
         g._csr_cache = self._csr_cache  # structure is shared, so is its device CSR
         g._host_csr = self._host_csr
         g._complete = getattr(self, "_complete", None)
+        g._kdeg = getattr(self, "_kdeg", None)
         return g
 
     def cuda(self, device=None) -> "RobotGraph":
@@ -171,9 +172,24 @@ class RobotGraph:
             self._complete = is_complete_batch(self._src.numpy(), self._dst.numpy(), self._bnn)
         return self._complete
 
-    def csr(self, device, allow_complete: bool = True) -> GraphCSR:
+    def in_degree_k(self) -> int:
+        """k when every node has exactly k in-edges (k-NN frames), else 0."""
+        if getattr(self, "_kdeg", None) is None:
+            deg = np.diff(self.host_csr()[0])
+            self._kdeg = int(deg[0]) if deg.size and deg[0] > 0 and np.all(deg == deg[0]) else 0
+        return self._kdeg
+
+    def csr(self, device, allow_complete: bool = True, allow_regular: bool = True) -> GraphCSR:
+        """Device CSR for the kernels.  ``graph_kind`` is GRAPH_COMPLETE for the reference topology,
+        ``graph_regular(k)`` when every node has k in-edges (k <= 8; the backward then keeps one
+        Gram accumulator per edge), else GRAPH_CSR."""
         device = torch.device(device)
-        kind = GRAPH_COMPLETE if (allow_complete and self.is_complete()) else GRAPH_CSR
+        if allow_complete and self.is_complete():
+            kind = GRAPH_COMPLETE
+        elif allow_regular and 1 <= self.in_degree_k() <= MAX_REGULAR_K:
+            kind = graph_regular(self.in_degree_k())
+        else:
+            kind = GRAPH_CSR
         key = (str(device), kind)
         hit = self._csr_cache.get(key)
         if hit is not None:

@@ -329,6 +329,49 @@ def test_complete_fast_path_equals_csr_path(cuda_device, n, hw):
     assert rel_err(res[0][2].numpy(), res[1][2].numpy()) <= 1e-6
 
 
+def regular_graph(n, k, rng, multi=False):
+    """Every node has exactly k in-edges from random sources (repeats allowed when ``multi``)."""
+    src, dst = [], []
+    for v in range(n):
+        us = rng.randint(0, n, k) if multi else rng.permutation(n)[:k]
+        src += [int(u) for u in us]
+        dst += [v] * k
+    return m.graph((src, dst), num_nodes=n)
+
+
+@pytest.mark.parametrize("n,k", [(9, 1), (10, 3), (12, 4), (16, 4), (16, 5), (13, 8), (16, 8)])
+@pytest.mark.parametrize("hw", [(8, 8), (3, 5)])
+@pytest.mark.parametrize("multi", [False, True])
+def test_regular_backward_equals_csr_path(cuda_device, n, k, hw, multi):
+    """The per-edge-slot backward of regular graphs (film_bwd_regular) against the oracle and the
+    general CSR kernels, for mixed graph sizes, multi-edges/self-loops and both slice widths."""
+    rng = np.random.RandomState(n * 31 + k)
+    small = max(k, n - 3)
+    g = m.batch([regular_graph(n, k, rng, multi), regular_graph(small, k, rng, multi), regular_graph(n, k, rng, multi)])
+    assert g.in_degree_k() == k
+    fast, slow = g.csr(cuda_device), g.csr(cuda_device, allow_regular=False)
+    assert fast.graph_kind == m.graph_regular(k) and slow.graph_kind == 0
+    torch.manual_seed(n + k)
+    x = torch.randn(g.num_nodes(), 12, *hw)
+    z = torch.randn(g.num_edges(), 12, 2)
+    G = torch.randn_like(x)
+    src, dst = (t.numpy() for t in g.edges())
+    dx_ref, dgb_ref = oracle.film_aggregate_grads(x, torch.sigmoid(z), src, dst, G)
+    res = []
+    for csr in (fast, slow):
+        xd = x.to(cuda_device).requires_grad_(True)
+        zd = z.to(cuda_device).requires_grad_(True)
+        out = m.film_mean_cat(xd, zd, csr, logits=True)
+        out.backward(torch.cat((G, G), 1).to(cuda_device))
+        res.append((out.detach().cpu(), xd.grad.cpu(), zd.grad.cpu()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert rel_err(res[0][1].numpy(), (dx_ref + G).numpy()) <= TOL
+    dz_ref = dgb_ref * torch.sigmoid(z) * (1 - torch.sigmoid(z))
+    assert rel_err(res[0][2].numpy(), dz_ref.numpy()) <= TOL
+    assert rel_err(res[0][1].numpy(), res[1][1].numpy()) <= 1e-6
+    assert rel_err(res[0][2].numpy(), res[1][2].numpy()) <= 1e-6
+
+
 @pytest.mark.parametrize("complete", [True, False])
 def test_cat_fused_forward_backward(cuda_device, complete):
     """film_mean_cat == torch.cat((x, film_mean(x)), 1), forward exactly, backward (incl. the

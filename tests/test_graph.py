@@ -111,10 +111,22 @@ def test_is_complete_detection():
     frames = [m.frame_graph(rng.randn(5, 7)) for _ in range(3)]
     assert m.batch(frames).is_complete()
     assert m.batch(frames).csr("cpu").graph_kind == 1
-    assert m.batch(frames).csr("cpu", allow_complete=False).graph_kind == 0
+    assert m.batch(frames).csr("cpu", allow_complete=False, allow_regular=False).graph_kind == 0
+    # without the complete fast path a complete graph is still regular: in-degree n-1
+    assert m.batch(frames).csr("cpu", allow_complete=False).graph_kind == m.graph_regular(4)
     assert not m.batch([m.complete_graph(5), m.complete_graph(4)]).is_complete()  # ragged
     assert not m.frame_graph(rng.randn(6, 7), knn=3).is_complete()
     assert m.batch([m.complete_graph(1), m.complete_graph(1)]).is_complete()
     # same edge set, different edge order -> not the arithmetic numbering
     s, d = m.complete_edges(4)
     assert not m.graph((s[::-1], d[::-1]), num_nodes=4).is_complete()
+
+
+def test_regular_degree_detection():
+    rng = np.random.RandomState(1)
+    knn = m.batch([m.frame_graph(rng.randn(12, 7), knn=4), m.frame_graph(rng.randn(9, 7), knn=4)])
+    assert knn.in_degree_k() == 4 and knn.csr("cpu").graph_kind == m.graph_regular(4) == (4 << 8) | 2
+    assert m.batch([m.frame_graph(rng.randn(12, 7), knn=4), m.frame_graph(rng.randn(9, 7), knn=3)]).in_degree_k() == 0
+    wide = m.frame_graph(rng.randn(14, 7), knn=9)  # in-degree above the per-edge-slot limit
+    assert wide.in_degree_k() == 9 and wide.csr("cpu").graph_kind == 0
+    assert m.graph(([0, 1], [1, 1]), num_nodes=2).in_degree_k() == 0  # node 0 has no in-edge

@@ -301,24 +301,60 @@ int main(int argc, char** argv) {
     BVAR(2, 4)
     CK(hipFree(dgb));
   }
+  if (KNN >= 1 && KNN <= 4 && N > 8) {
+    // regular (per-edge-slot) backward: lanes per channel plane x slice width
+    float* dgb;
+    CK(hipMalloc(&dgb, (size_t)E * C * 2 * 4));
+    const double bwd_bytes = (double)feat * 12 + (double)E * C * 2 * 8;
+    auto rargs = [&](int vec, int lpc) {
+      mrp::AggArgs a = {};
+      const int cpb = std::min(16, 256 / lpc);
+      a.x = x; a.xs = (int64_t)C * P; a.g = gout; a.gs = (int64_t)C * P; a.gb = gb; a.goff = d_goff;
+      a.indptr = d_indptr; a.src = d_src; a.eid = d_eid; a.out = out; a.os = (int64_t)C * P; a.dgb = dgb;
+      a.C = C; a.P = P; a.PV = P / vec; a.mode = 0; a.lpc = lpc; a.cpb = cpb; a.ncb = (C + cpb - 1) / cpb;
+      a.want_dx = 1; a.want_dgb = 1; a.logits = 1; a.kdeg = KNN;
+      return a;
+    };
+#define RVAR(NT, VEC, LPC)                                                                               \
+    if (N == NT) {                                                                                       \
+      mrp::AggArgs a = rargs(VEC, LPC);                                                                  \
+      const size_t lds_ = lds_regular<NT, 4>(a.cpb);                                                     \
+      float ms_ = time_ms([&] { hipLaunchKernelGGL((mrp::film_bwd_regular<NT, 4, VEC, false>),           \
+                                                   dim3(B * a.ncb), dim3(a.cpb * LPC), lds_, 0, a); }, iters); \
+      char nm_[96];                                                                                      \
+      snprintf(nm_, sizeof nm_, "bwd_regular<%d> vec=%d lpc=%d cpb=%d", NT, VEC, LPC, a.cpb);           \
+      report(nm_, ms_, bwd_bytes);                                                                       \
+    }
+    RVAR(16, 2, 64)
+    RVAR(16, 2, 32)
+    RVAR(16, 2, 16)
+    RVAR(16, 2, 8)
+    RVAR(16, 1, 64)
+    RVAR(16, 1, 32)
+    RVAR(16, 1, 16)
+    RVAR(16, 1, 8)
+    CK(hipFree(dgb));
+  }
   // product entry points (default geometry), both graph kinds
   float* dgb_prod;
   CK(hipMalloc(&dgb_prod, (size_t)E * C * 2 * 4));
-  for (int kind : {MRP_GRAPH_CSR, MRP_GRAPH_COMPLETE}) {
+  for (int kind : {(int)MRP_GRAPH_CSR, (int)MRP_GRAPH_COMPLETE, (int)MRP_GRAPH_REGULAR(KNN)}) {
     if (KNN && kind == MRP_GRAPH_COMPLETE) continue;
+    if (!KNN && MRP_GRAPH_IS_REGULAR(kind)) continue;
     char nm[96];
     float ms = time_ms([&] {
       CK((hipError_t)mrp_film_mean_fwd(x, (int64_t)C * P, gb, d_indptr, d_src, d_eid, d_goff, B, N, kind, Nt, E, C,
                                        P, 0, out, (int64_t)C * P, nullptr));
     }, iters);
-    snprintf(nm, sizeof nm, "mrp_film_mean_fwd kind=%s", kind ? "complete" : "csr");
+    const char* kn = kind == MRP_GRAPH_CSR ? "csr" : kind == MRP_GRAPH_COMPLETE ? "complete" : "regular";
+    snprintf(nm, sizeof nm, "mrp_film_mean_fwd kind=%s", kn);
     report(nm, ms, alg);
     ms = time_ms([&] {
       CK((hipError_t)mrp_film_mean_bwd(gout, (int64_t)C * P, x, (int64_t)C * P, gb, d_indptr, d_src, d_eid, d_goff, B,
                                        N, kind, Nt, E, C, P, MRP_AGG_GB_LOGITS, out, (int64_t)C * P, nullptr, 0,
                                        dgb_prod, nullptr));
     }, iters);
-    snprintf(nm, sizeof nm, "mrp_film_mean_bwd kind=%s (dx+dgb)", kind ? "complete" : "csr");
+    snprintf(nm, sizeof nm, "mrp_film_mean_bwd kind=%s (dx+dgb)", kn);
     // bwd alg bytes: read G and x, write dx, read gb, write dgb
     report(nm, ms, (double)feat * 12 + (double)E * C * 2 * 8);
   }
