@@ -32,6 +32,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 
 #include "mrp_gnn.h"
 
@@ -858,13 +859,15 @@ struct Geometry {
 };
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
 
-Geometry make_geometry(int C, int P, int vec) {
+// lanes per channel plane: the largest power of two <= min(max_lpc, P / vec)
+Geometry make_geometry(int C, int P, int vec, int max_lpc) {
   Geometry g;
   g.vec = vec;
   const int pv = P / g.vec;
   int lpc = 1;
-  while (lpc * 2 <= pv && lpc * 2 <= 64) lpc *= 2;
+  while (lpc * 2 <= pv && lpc * 2 <= max_lpc) lpc *= 2;
   int cpb = mrp::kBlock / lpc;
   if (cpb > mrp::kMaxChanPerBlock) cpb = mrp::kMaxChanPerBlock;
   if (cpb > C) cpb = C;
@@ -902,8 +905,12 @@ hipError_t launch_fwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
   const size_t lds = lds_fwd<NT>(g.cpb);
   if (g.vec == 4)
     MRP_LAUNCH((mrp::film_fwd<NT, 4, COMPLETE>), lds);
-  else
+  else if (g.vec == 2)
+    MRP_LAUNCH((mrp::film_fwd<NT, 2, COMPLETE>), lds);
+  else if (g.vec == 1)
     MRP_LAUNCH((mrp::film_fwd<NT, 1, COMPLETE>), lds);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -953,7 +960,7 @@ hipError_t launch_bwd_regular(const AggArgs& a, const Geometry& g, hipStream_t s
   // VEC 4 would need 4*NT registers more per operand and spills; KMAX 8 only fits at VEC 1
   const size_t lds = lds_regular<NT, KMAX>(g.cpb);
   if constexpr (KMAX <= 4) {
-    if (g.vec >= 2) {
+    if (g.vec == 2) {
       MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 2, DXB>), lds);
       return hipGetLastError();
     }
@@ -1049,7 +1056,11 @@ int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, co
   if (mode != MRP_AGG_COPY_MEAN && num_edges > 0 && gb == nullptr) return hipErrorInvalidValue;
   const bool vec4 =
       (P % 4 == 0) && (x_node_stride % 4 == 0) && (out_node_stride % 4 == 0) && aligned16(x) && aligned16(out);
-  Geometry g = make_geometry(C, P, vec4 ? 4 : 1);
+  // at least two slices per lane: 64 lanes per plane at the north-star size (P=1024), 32 for
+  // 16x16 planes (228 vs 248 us at k-NN(4) N=16 C=1024); 16-byte slices beat 8-byte ones at both
+  // (tools/kernel_lab.hip product sweep)
+  const int vec = vec4 ? 4 : 1;
+  Geometry g = make_geometry(C, P, vec, std::max(1, std::min(64, P / vec / 2)));
   g.grid = (int64_t)num_graphs * g.ncb;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
   AggArgs a = {};
@@ -1108,9 +1119,15 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   // 16-byte slices: with the DPP lane reduction they beat 8-byte slices (310 vs 322 us at B=32,
   // N=8, C=512, 32x32) despite 2 waves/SIMD instead of 3.  VEC=2 stays compiled for experiments.
   int vec = vec4 ? 4 : 1;
+  int max_lpc = 64;
   const int kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
-  if (max_nodes > 8 && kdeg >= 1 && kdeg <= 8) vec = (vec4 && kdeg <= 4) ? 2 : 1;  // film_bwd_regular
-  Geometry g = make_geometry(C, P, vec);
+  if (max_nodes > 8 && kdeg >= 1 && kdeg <= 8) {
+    // film_bwd_regular: 8-byte slices on 16 lanes per plane (367 us against 569 us on 64 lanes at
+    // k-NN(4) N=16 C=1024 16x16): its prologue and lane reduction are amortised over more slices
+    vec = (vec4 && kdeg <= 4) ? 2 : 1;
+    max_lpc = vec == 2 ? 16 : 32;
+  }
+  Geometry g = make_geometry(C, P, vec, max_lpc);
   g.grid = (int64_t)num_graphs * g.ncb;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
   AggArgs a = {};

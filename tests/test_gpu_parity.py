@@ -314,7 +314,7 @@ def test_complete_fast_path_equals_csr_path(cuda_device, n, hw):
     the forward and to rounding on the backward."""
     g, x, gb = random_case(n, 12, hw[0], hw[1], seed=200 + n, bnn=[n] * 3)
     assert g.is_complete()
-    fast, slow = g.csr(cuda_device), g.csr(cuda_device, allow_complete=False)
+    fast, slow = g.csr(cuda_device), g.csr(cuda_device, allow_complete=False, allow_regular=False)
     assert fast.graph_kind == 1 and slow.graph_kind == 0
     G = torch.randn_like(x).to(cuda_device)
     res = []

@@ -26,7 +26,8 @@
 namespace lab {
 using mrp::f4;
 
-__global__ void __launch_bounds__(256) stream_copy(const f4* __restrict__ in, f4* __restrict__ out, size_t n) {
+template <typename T>
+__global__ void __launch_bounds__(256) stream_copy(const T* __restrict__ in, T* __restrict__ out, size_t n) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (; i < n; i += stride) out[i] = in[i];
@@ -214,9 +215,13 @@ int main(int argc, char** argv) {
     const size_t n4 = feat / 4;
     for (int grid : {1024, 2048, 4096, 8192}) {
       char nm[64];
-      snprintf(nm, sizeof nm, "stream_copy grid=%d", grid);
-      float ms = time_ms([&] { hipLaunchKernelGGL(lab::stream_copy, dim3(grid), dim3(256), 0, 0,
+      snprintf(nm, sizeof nm, "stream_copy f4 grid=%d", grid);
+      float ms = time_ms([&] { hipLaunchKernelGGL(lab::stream_copy<mrp::f4>, dim3(grid), dim3(256), 0, 0,
                                                   (const mrp::f4*)x, (mrp::f4*)out, n4); }, iters);
+      report(nm, ms, (double)feat * 8);
+      snprintf(nm, sizeof nm, "stream_copy f2 grid=%d", grid);
+      ms = time_ms([&] { hipLaunchKernelGGL(lab::stream_copy<mrp::f2>, dim3(grid), dim3(256), 0, 0,
+                                            (const mrp::f2*)x, (mrp::f2*)out, n4 * 2); }, iters);
       report(nm, ms, (double)feat * 8);
     }
   }
@@ -333,6 +338,45 @@ int main(int argc, char** argv) {
     RVAR(16, 1, 32)
     RVAR(16, 1, 16)
     RVAR(16, 1, 8)
+    CK(hipFree(dgb));
+  }
+  {
+    // product dispatch at forced geometries: lanes per channel plane (cpb = min(16, 256/lpc))
+    float* dgb;
+    CK(hipMalloc(&dgb, (size_t)E * C * 2 * 4));
+    const double bwd_bytes = (double)feat * 12 + (double)E * C * 2 * 8;
+    const int kind = KNN ? (int)MRP_GRAPH_REGULAR(KNN) : (int)MRP_GRAPH_COMPLETE;
+    for (int bwd = 0; bwd < 2; ++bwd) {
+      for (int vec : {4, 2, 1}) {
+        for (int lpc : {64, 32, 16}) {
+          if (bwd && KNN && N > 8 && vec == 4) continue;  // the regular kernel has no 16-byte variant
+          if (bwd && !(KNN && N > 8) && vec == 2) continue;
+          Geometry g;
+          g.vec = vec;
+          g.lpc = lpc;
+          g.cpb = std::min(16, 256 / lpc);
+          g.threads = g.cpb * lpc;
+          g.ncb = (C + g.cpb - 1) / g.cpb;
+          g.grid = (int64_t)B * g.ncb;
+          mrp::AggArgs a = {};
+          a.x = x; a.xs = (int64_t)C * P; a.gb = gb; a.indptr = d_indptr; a.src = d_src; a.eid = d_eid;
+          a.goff = d_goff; a.out = out; a.os = (int64_t)C * P; a.C = C; a.P = P; a.PV = P / vec; a.mode = 0;
+          a.lpc = g.lpc; a.cpb = g.cpb; a.ncb = g.ncb; a.logits = 1;
+          if (bwd) {
+            a.g = gout; a.gs = (int64_t)C * P; a.dgb = dgb; a.want_dx = 1; a.want_dgb = 1;
+            a.kdeg = KNN;
+          }
+          float ms = time_ms([&] {
+            CK(bwd ? dispatch_bwd(N, kind == MRP_GRAPH_COMPLETE, a, g, nullptr)
+                   : dispatch_fwd(N, kind == MRP_GRAPH_COMPLETE, a, g, nullptr));
+          }, iters);
+          char nm[96];
+          snprintf(nm, sizeof nm, "%s vec=%d lpc=%d cpb=%d grid=%lld", bwd ? "bwd" : "fwd", vec, lpc, g.cpb,
+                   (long long)g.grid);
+          report(nm, ms, bwd ? bwd_bytes : alg);
+        }
+      }
+    }
     CK(hipFree(dgb));
   }
   // product entry points (default geometry), both graph kinds
