@@ -861,15 +861,20 @@ struct Geometry {
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
 
-// lanes per channel plane: the largest power of two <= min(max_lpc, P / vec)
-Geometry make_geometry(int C, int P, int vec, int max_lpc) {
+// Lanes per channel plane: the largest power of two <= clamp(P/vec/2, lo, hi) (two slices per lane
+// where the plane allows) and <= P/vec; channels per block fill the 256 threads up to max_cpb.
+// Measured optima (tools/kernel_lab.hip product sweep): forward lo=16, hi=64 (64 lanes at 32x32,
+// 32 at 16x16, 16 at 8x8); fused backward lo=8 (8 lanes x 32 channels at 8x8: 78 vs 87 us at
+// C=1280); regular backward 16.
+Geometry make_geometry(int C, int P, int vec, int lo, int hi, int max_cpb) {
   Geometry g;
   g.vec = vec;
   const int pv = P / g.vec;
+  const int target = std::min(std::max(pv / 2, lo), hi);
   int lpc = 1;
-  while (lpc * 2 <= pv && lpc * 2 <= max_lpc) lpc *= 2;
+  while (lpc * 2 <= pv && lpc * 2 <= target) lpc *= 2;
   int cpb = mrp::kBlock / lpc;
-  if (cpb > mrp::kMaxChanPerBlock) cpb = mrp::kMaxChanPerBlock;
+  if (cpb > max_cpb) cpb = max_cpb;
   if (cpb > C) cpb = C;
   g.lpc = lpc;
   g.cpb = cpb;
@@ -1056,11 +1061,8 @@ int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, co
   if (mode != MRP_AGG_COPY_MEAN && num_edges > 0 && gb == nullptr) return hipErrorInvalidValue;
   const bool vec4 =
       (P % 4 == 0) && (x_node_stride % 4 == 0) && (out_node_stride % 4 == 0) && aligned16(x) && aligned16(out);
-  // at least two slices per lane: 64 lanes per plane at the north-star size (P=1024), 32 for
-  // 16x16 planes (228 vs 248 us at k-NN(4) N=16 C=1024); 16-byte slices beat 8-byte ones at both
-  // (tools/kernel_lab.hip product sweep)
-  const int vec = vec4 ? 4 : 1;
-  Geometry g = make_geometry(C, P, vec, std::max(1, std::min(64, P / vec / 2)));
+  // 16-byte slices beat 8-byte ones at every measured size (tools/kernel_lab.hip product sweep)
+  Geometry g = make_geometry(C, P, vec4 ? 4 : 1, 16, 64, mrp::kMaxChanPerBlock);
   g.grid = (int64_t)num_graphs * g.ncb;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
   AggArgs a = {};
@@ -1119,15 +1121,19 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   // 16-byte slices: with the DPP lane reduction they beat 8-byte slices (310 vs 322 us at B=32,
   // N=8, C=512, 32x32) despite 2 waves/SIMD instead of 3.  VEC=2 stays compiled for experiments.
   int vec = vec4 ? 4 : 1;
-  int max_lpc = 64;
+  Geometry g;
   const int kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
   if (max_nodes > 8 && kdeg >= 1 && kdeg <= 8) {
     // film_bwd_regular: 8-byte slices on 16 lanes per plane (367 us against 569 us on 64 lanes at
     // k-NN(4) N=16 C=1024 16x16): its prologue and lane reduction are amortised over more slices
     vec = (vec4 && kdeg <= 4) ? 2 : 1;
-    max_lpc = vec == 2 ? 16 : 32;
+    g = vec == 2 ? make_geometry(C, P, 2, 16, 16, mrp::kMaxChanPerBlock)
+                 : make_geometry(C, P, 1, 32, 32, mrp::kMaxChanPerBlock);
+  } else if (max_nodes <= 8) {
+    g = make_geometry(C, P, vec, 8, 64, 32);  // film_bwd_fused
+  } else {
+    g = make_geometry(C, P, vec, 64, 64, mrp::kMaxChanPerBlock);  // film_bwd_dx + Gram pass
   }
-  Geometry g = make_geometry(C, P, vec, max_lpc);
   g.grid = (int64_t)num_graphs * g.ncb;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
   AggArgs a = {};

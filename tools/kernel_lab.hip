@@ -348,13 +348,14 @@ int main(int argc, char** argv) {
     const int kind = KNN ? (int)MRP_GRAPH_REGULAR(KNN) : (int)MRP_GRAPH_COMPLETE;
     for (int bwd = 0; bwd < 2; ++bwd) {
       for (int vec : {4, 2, 1}) {
-        for (int lpc : {64, 32, 16}) {
+        for (int lpc : {64, 32, 16, 8, 4}) {
           if (bwd && KNN && N > 8 && vec == 4) continue;  // the regular kernel has no 16-byte variant
           if (bwd && !(KNN && N > 8) && vec == 2) continue;
+          if (lpc > P / vec) continue;
           Geometry g;
           g.vec = vec;
           g.lpc = lpc;
-          g.cpb = std::min(16, 256 / lpc);
+          g.cpb = std::min(C, 256 / lpc);
           g.threads = g.cpb * lpc;
           g.ncb = (C + g.cpb - 1) / g.cpb;
           g.grid = (int64_t)B * g.ncb;
