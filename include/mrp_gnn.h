@@ -100,6 +100,21 @@ int mrp_film_mean_fwd(const float* x, int64_t x_node_stride,
                       void* stream);
 
 /*
+ * torch.cat((x, update_all(...)), 1) in one pass (dgl/model/models.py:181-182, 186-188): as
+ * mrp_film_mean_fwd, but `cat` is the (num_nodes, 2C, P) concatenation buffer (node stride
+ * cat_node_stride >= 2*C*P): x is written to channels [0, C) and the aggregate to [C, 2C).  The
+ * kernel stores the slices of x it already holds in registers, so x is read once instead of twice.
+ */
+int mrp_film_mean_cat_fwd(const float* x, int64_t x_node_stride,
+                          const float* gb,
+                          const int32_t* indptr, const int32_t* src, const int32_t* eid,
+                          const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes,
+                          int32_t graph_kind, int32_t num_nodes, int32_t num_edges,
+                          int32_t C, int32_t P, int32_t mode,
+                          float* cat, int64_t cat_node_stride,
+                          void* stream);
+
+/*
  * Backward of mrp_film_mean_fwd (the autograd of models.py:207-211 through DGL's
  * gather/mailbox, which the reference gets from torch autograd).  With s_v the
  * reduce scale (1/deg v for the mean modes, 1 for SUM) and G = grad_out:

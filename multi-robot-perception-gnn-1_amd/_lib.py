@@ -20,12 +20,13 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
 #: Every symbol ``include/mrp_gnn.h`` declares.
 EXPORTED_SYMBOLS = (
     "mrp_film_mean_fwd",
+    "mrp_film_mean_cat_fwd",
     "mrp_film_mean_bwd",
     "mrp_edge_hidden_fwd",
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_NODES = 16
 
 MODE_FILM_MEAN = 0
@@ -56,6 +57,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     graph = [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32]  # indptr..mode
     lib.mrp_film_mean_fwd.argtypes = [_P, _I64, _P] + graph + [_P, _I64, _P]
     lib.mrp_film_mean_fwd.restype = ctypes.c_int
+    lib.mrp_film_mean_cat_fwd.argtypes = [_P, _I64, _P] + graph + [_P, _I64, _P]
+    lib.mrp_film_mean_cat_fwd.restype = ctypes.c_int
     lib.mrp_film_mean_bwd.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _I64, _P, _P]
     lib.mrp_film_mean_bwd.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]

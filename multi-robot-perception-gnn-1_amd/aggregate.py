@@ -63,12 +63,24 @@ def film_mean_forward_into(x: torch.Tensor, gb: Optional[torch.Tensor], csr: Gra
                            out: torch.Tensor) -> torch.Tensor:
     """Run the forward kernel into ``out`` (N, C, H, W) — which may be a strided view such as
     the second half of a ``torch.cat((h, g_h), 1)`` buffer.  No autograd."""
+    return _forward(x, gb, csr, mode, out, cat=False)
+
+
+def film_mean_cat_forward_into(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode: int,
+                               cat: torch.Tensor) -> torch.Tensor:
+    """``cat[:, :C] = x; cat[:, C:] = film_mean(x)`` for a (N, 2C, H, W) buffer, one kernel pass
+    (``mrp_film_mean_cat_fwd``).  No autograd."""
+    return _forward(x, gb, csr, mode, cat, cat=True)
+
+
+def _forward(x, gb, csr, mode, out, cat):
     _require_device(x, out)
     n, C, H, W = x.shape
     x, xs = _as_node_major(x)
     os_ = node_stride(out)
-    if os_ is None or tuple(out.shape) != (n, C, H, W):
-        raise ValueError("out must be (N, C, H, W) fp32 with a contiguous C*H*W block per node")
+    want = (n, 2 * C, H, W) if cat else (n, C, H, W)
+    if os_ is None or tuple(out.shape) != want:
+        raise ValueError(f"out must be {want} fp32 with a contiguous block per node")
     if (mode & ~_lib.GB_LOGITS) != _lib.MODE_COPY_MEAN:
         if gb is None:
             raise ValueError("gamma/beta tensor required for FiLM modes")
@@ -81,12 +93,13 @@ def film_mean_forward_into(x: torch.Tensor, gb: Optional[torch.Tensor], csr: Gra
     if n != csr.num_nodes:
         raise ValueError(f"x has {n} nodes, graph has {csr.num_nodes}")
     lib = _lib.load_library()
+    fn = lib.mrp_film_mean_cat_fwd if cat else lib.mrp_film_mean_fwd
     with torch.cuda.device(x.device):
-        code = lib.mrp_film_mean_fwd(
+        code = fn(
             _ptr(x), xs, _ptr(gb), _ptr(csr.indptr), _ptr(csr.src), _ptr(csr.eid), _ptr(csr.graph_off),
             csr.num_graphs, csr.max_nodes, csr.graph_kind, csr.num_nodes, csr.num_edges, C, H * W, mode,
             _ptr(out), os_, _stream(x.device))
-    _lib.check(code, "mrp_film_mean_fwd")
+    _lib.check(code, "mrp_film_mean_cat_fwd" if cat else "mrp_film_mean_fwd")
     return out
 
 
@@ -167,16 +180,15 @@ def film_mean(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="
 
 class FilmMeanCatFunction(torch.autograd.Function):
     """``torch.cat((x, film_mean(x, gb)), 1)`` without the concatenation pass for the aggregate
-    (``dgl/model/models.py:181-182,187-188``): the kernel writes straight into the second half of the
-    (N, 2C, H, W) buffer; backward hands the kernel the second half of the incoming gradient as
+    (``dgl/model/models.py:181-182,187-188``): the kernel writes the aggregate into the second half of
+    the (N, 2C, H, W) buffer and x, whose slices it holds anyway, into the first; backward hands the kernel the second half of the incoming gradient as
     grad_out and the first half as the base of x's gradient."""
 
     @staticmethod
     def forward(ctx, x, gb, csr: GraphCSR, mode: int):
         n, C, H, W = x.shape
         buf = torch.empty((n, 2 * C, H, W), device=x.device, dtype=torch.float32)
-        buf[:, :C].copy_(x)
-        film_mean_forward_into(x, gb, csr, mode, buf[:, C:])
+        film_mean_cat_forward_into(x, gb, csr, mode, buf)  # the kernel also writes x into buf[:, :C]
         ctx.save_for_backward(x, gb)
         ctx.csr = csr
         ctx.mode = mode

@@ -66,6 +66,8 @@ struct AggArgs {
   int32_t want_dx, want_dgb;
   int32_t logits;  // gb holds pre-sigmoid logits (MRP_AGG_GB_LOGITS): apply sigmoid on load
   int32_t kdeg;    // MRP_GRAPH_REGULAR: every node's in-degree (else 0)
+  float* xc;       // forward: optional copy of x (the first half of a concatenation buffer)
+  int64_t xcs;     // its node stride
 };
 
 __device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
@@ -390,6 +392,16 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
         for (int k = 0; k < VEC; ++k) acc.v[k] = acc.v[k] / d;
       }
       store_frag<VEC, true>(ob + (int64_t)v * a.os + off, acc);
+    }
+    if (a.xc != nullptr) {
+      // cat((x, aggregate), 1): the slices of x are in registers already; writing them here saves
+      // the separate copy's read of x
+      float* xcb = a.xc + (int64_t)node0 * a.xcs + (int64_t)c * a.P + off;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        if (u >= n) break;
+        store_frag<VEC, true>(xcb + (int64_t)u * a.xcs, xv[u]);
+      }
     }
     j += a.lpc;
     if (j < a.PV) {
@@ -1041,14 +1053,18 @@ bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* ei
 
 extern "C" {
 
-int mrp_abi_version(void) { return 6; }
+int mrp_abi_version(void) { return 7; }
 
 const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
 
-int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr,
-                      const int32_t* src, const int32_t* eid, const int32_t* graph_off, int32_t num_graphs,
-                      int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C,
-                      int32_t P, int32_t mode_flags, float* out, int64_t out_node_stride, void* stream) {
+}  // extern "C"
+
+namespace {
+
+int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr, const int32_t* src,
+                  const int32_t* eid, const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes,
+                  int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode_flags,
+                  float* out, int64_t out_node_stride, float* xcopy, int64_t xcopy_node_stride, void* stream) {
   const int32_t logits = (mode_flags & MRP_AGG_GB_LOGITS) ? 1 : 0;
   const int32_t mode = mode_flags & ~MRP_AGG_GB_LOGITS;
   if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind, num_nodes, num_edges, C, P,
@@ -1059,8 +1075,10 @@ int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, co
   if (x == nullptr || out == nullptr || x_node_stride < plane || out_node_stride < plane)
     return hipErrorInvalidValue;
   if (mode != MRP_AGG_COPY_MEAN && num_edges > 0 && gb == nullptr) return hipErrorInvalidValue;
-  const bool vec4 =
+  if (xcopy != nullptr && xcopy_node_stride < plane) return hipErrorInvalidValue;
+  bool vec4 =
       (P % 4 == 0) && (x_node_stride % 4 == 0) && (out_node_stride % 4 == 0) && aligned16(x) && aligned16(out);
+  if (xcopy != nullptr) vec4 = vec4 && (xcopy_node_stride % 4 == 0) && aligned16(xcopy);
   // 16-byte slices beat 8-byte ones at every measured size (tools/kernel_lab.hip product sweep)
   Geometry g = make_geometry(C, P, vec4 ? 4 : 1, 16, 64, mrp::kMaxChanPerBlock);
   g.grid = (int64_t)num_graphs * g.ncb;
@@ -1083,7 +1101,31 @@ int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, co
   a.cpb = g.cpb;
   a.ncb = g.ncb;
   a.logits = logits;
+  a.xc = xcopy;
+  a.xcs = xcopy_node_stride;
   return dispatch_fwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, static_cast<hipStream_t>(stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr,
+                      const int32_t* src, const int32_t* eid, const int32_t* graph_off, int32_t num_graphs,
+                      int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C,
+                      int32_t P, int32_t mode_flags, float* out, int64_t out_node_stride, void* stream) {
+  return film_fwd_impl(x, x_node_stride, gb, indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind,
+                       num_nodes, num_edges, C, P, mode_flags, out, out_node_stride, nullptr, 0, stream);
+}
+
+int mrp_film_mean_cat_fwd(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr,
+                          const int32_t* src, const int32_t* eid, const int32_t* graph_off, int32_t num_graphs,
+                          int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C,
+                          int32_t P, int32_t mode_flags, float* cat, int64_t cat_node_stride, void* stream) {
+  if (cat == nullptr || cat_node_stride < 2 * (int64_t)C * P) return hipErrorInvalidValue;
+  return film_fwd_impl(x, x_node_stride, gb, indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind,
+                       num_nodes, num_edges, C, P, mode_flags, cat + (int64_t)C * P, cat_node_stride, cat,
+                       cat_node_stride, stream);
 }
 
 int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float* x, int64_t x_node_stride,

@@ -373,10 +373,13 @@ def test_regular_backward_equals_csr_path(cuda_device, n, k, hw, multi):
 
 
 @pytest.mark.parametrize("complete", [True, False])
-def test_cat_fused_forward_backward(cuda_device, complete):
-    """film_mean_cat == torch.cat((x, film_mean(x)), 1), forward exactly, backward (incl. the
-    grad_x_base accumulation of the concatenation's first half) to rounding."""
-    g, x, gb = random_case(8, 16, 8, 8, seed=31, bnn=[8, 8, 8])
+@pytest.mark.parametrize("bnn,hw,knn", [([8, 8, 8], (8, 8), None), ([8, 5, 3, 1], (3, 5), None),
+                                        ([12, 16, 9], (4, 4), 3), ([16, 7], (1, 1), None)])
+def test_cat_fused_forward_backward(cuda_device, complete, bnn, hw, knn):
+    """film_mean_cat == torch.cat((x, film_mean(x)), 1), forward exactly (the kernel writes both
+    halves: mrp_film_mean_cat_fwd), backward (incl. the grad_x_base accumulation of the
+    concatenation's first half) to rounding; ragged, k-NN, odd and 1x1 planes."""
+    g, x, gb = random_case(max(bnn), 16, hw[0], hw[1], seed=31, bnn=bnn, knn=knn)
     csr = g.csr(cuda_device, allow_complete=complete)
     x1 = x.to(cuda_device).requires_grad_(True)
     x2 = x.to(cuda_device).requires_grad_(True)
@@ -390,3 +393,16 @@ def test_cat_fused_forward_backward(cuda_device, complete):
     b.backward(G)
     assert rel_err(x1.grad.cpu().numpy(), x2.grad.cpu().numpy()) <= 1e-6
     assert rel_err(z1.grad.cpu().numpy(), z2.grad.cpu().numpy()) <= 1e-6
+
+
+def test_cat_forward_strided_source(cuda_device):
+    """x read through a node stride (a channel slice of a wider buffer), cat buffer written whole."""
+    g, x, gb = random_case(6, 8, 4, 4, seed=5, bnn=[6, 6])
+    wide = torch.randn(x.shape[0], 24, 4, 4)
+    wide[:, 4:12] = x
+    xd = wide.to(cuda_device)[:, 4:12]
+    assert not xd.is_contiguous()
+    buf = torch.full((x.shape[0], 16, 4, 4), float("nan"), device=cuda_device)
+    m.film_mean_cat_forward_into(xd, gb.to(cuda_device), g.csr(cuda_device), 0, buf)
+    ref = torch.cat((x, oracle.film_aggregate(x, gb, *[t.numpy() for t in g.edges()])), 1)
+    assert torch.equal(buf.cpu(), ref)

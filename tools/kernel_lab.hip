@@ -394,6 +394,17 @@ int main(int argc, char** argv) {
     const char* kn = kind == MRP_GRAPH_CSR ? "csr" : kind == MRP_GRAPH_COMPLETE ? "complete" : "regular";
     snprintf(nm, sizeof nm, "mrp_film_mean_fwd kind=%s", kn);
     report(nm, ms, alg);
+    {
+      float* catb;
+      CK(hipMalloc(&catb, (size_t)Nt * 2 * C * P * 4));
+      ms = time_ms([&] {
+        CK((hipError_t)mrp_film_mean_cat_fwd(x, (int64_t)C * P, gb, d_indptr, d_src, d_eid, d_goff, B, N, kind, Nt,
+                                             E, C, P, 0, catb, (int64_t)2 * C * P, nullptr));
+      }, iters);
+      snprintf(nm, sizeof nm, "mrp_film_mean_cat_fwd kind=%s", kn);
+      report(nm, ms, alg + (double)feat * 4);  // + the copy of x
+      CK(hipFree(catb));
+    }
     ms = time_ms([&] {
       CK((hipError_t)mrp_film_mean_bwd(gout, (int64_t)C * P, x, (int64_t)C * P, gb, d_indptr, d_src, d_eid, d_goff, B,
                                        N, kind, Nt, E, C, P, MRP_AGG_GB_LOGITS, out, (int64_t)C * P, nullptr, 0,
