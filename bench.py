@@ -162,6 +162,35 @@ def train_step_time(gcn, g, x, world, device, args):
     return t, nb
 
 
+def block_step_time(world, device, args, rank):
+    """BASELINE configs[1]: the 2-layer GCN of multi_view_dgl_model (compress_gcn + multi_gcn:
+    gcn1 -> cat -> conv1 -> gcn2 -> cat -> conv2, dgl/model/models.py:180-189) on B=16 8-robot
+    graphs, 512 x 32 x 32 features, forward.  Reported beside the north-star line, not as value."""
+    B, N, C, H = 16, 8, 512, 32
+    g = make_workload(B, N, C, H, H, seed=100 + rank, device=device)
+    opt = type("opt", (), {"feature_dim": C, "compress_gcn": True, "multi_gcn": True})()
+    torch.manual_seed(0)
+    block = mrp.GCNBlock(opt).to(device)
+    x = g.ndata["image"]
+    with torch.no_grad():
+        for _ in range(3):
+            block(g, x)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(args.block_steps):
+            block(g, x)
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+    t = max_over_ranks((time.perf_counter() - t0) / args.block_steps, world, device, args.dist_backend)
+    elems = 2 * g.num_nodes() * C * H * H  # two GCN layers
+    return {"config": "configs[1]: B=16/rank, N=8 complete, C=512, 32x32, 2 GCN layers with 1x1 compress "
+                      "(gcn1-cat-conv1-gcn2-cat-conv2), forward",
+            "value": world * elems / t, "unit": "elems/s", "ms_per_step": t * 1e3}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -177,6 +206,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step measurement")
     ap.add_argument("--train-steps", type=int, default=20)
+    ap.add_argument("--no-block", action="store_true", help="skip the configs[1] 2-layer block measurement")
+    ap.add_argument("--block-steps", type=int, default=10)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (control-flow tests)")
     args = ap.parse_args()
 
@@ -227,6 +258,7 @@ def main():
     train = None
     if not args.no_train:
         train = train_step_time(gcn, g, x, world, device, args)
+    block = None if args.no_block else block_step_time(world, device, args, rank)
 
     elems_per_step = Nt * C * P
     value = world * elems_per_step * args.steps / elapsed
@@ -263,6 +295,8 @@ def main():
             "value": world * elems_per_step / t_train, "unit": "elems/s", "ms_per_step": t_train * 1e3,
             "allreduce_buckets": reducer_buckets,
         }
+    if block is not None:
+        result["block_step"] = block
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(N, C, H, W, args.cpu_seconds, args.cpu_sample_graphs)
     if rank == 0:

@@ -7,7 +7,8 @@ Mirrors ``dgl/model/models.py``:
 * :class:`GCN`           — ``models.py:213-226``: ``forward(g)`` (the reference call, ``models.py:181``)
   and ``forward(g, feats)`` (the north-star signature).  Aggregation runs in the HIP kernel.
 * :class:`GCNBlock`      — the GCN stacking of ``multi_view_dgl_model.forward`` (``models.py:180-189``):
-  ``gcn1 -> cat -> [conv1] -> [gcn2 -> cat -> conv2]``, keys ``gcn1.*``, ``conv1.*``, ``gcn2.*``, ``conv2.*``.
+  ``gcn1 -> cat -> [conv1] -> [gcn2 -> cat -> conv2]``, keys ``gcn1.*``, ``conv1.*``, ``gcn2.*``, ``conv2.*``;
+  the 1x1 convs run as batched GEMMs (``compress.py``).
 * :class:`multi_view_dgl_model` — ``models.py:157-205`` with the CNN encoder/decoder supplied by the
   caller (they are torchvision/dense-conv code outside the hot path), so a reference
   ``encoder``/``decoder`` instance can be plugged in unchanged.
@@ -28,6 +29,7 @@ import torch
 import torch.nn as nn
 
 from .aggregate import film_mean, film_mean_cat
+from .compress import compress_1x1
 from .encoder import edge_logits
 
 
@@ -117,9 +119,9 @@ class GCNBlock(nn.Module):
     def forward(self, g, h: torch.Tensor) -> torch.Tensor:
         h = self.gcn1.forward_cat(g, h)  # cat((h, gcn1(h)), 1)
         if self.opt.compress_gcn:
-            h = self.conv1(h)
+            h = compress_1x1(self.conv1, h)
         if self.opt.multi_gcn:
-            h = self.conv2(self.gcn2.forward_cat(g, h))
+            h = compress_1x1(self.conv2, self.gcn2.forward_cat(g, h))
         return h
 
 
@@ -162,10 +164,10 @@ class multi_view_dgl_model(nn.Module):  # noqa: N801  (reference class name)
             g.ndata["image"] = h
             h = self.gcn1.forward_cat(g)  # cat((h, gcn1(g)), 1), models.py:181-182
             if self.opt.compress_gcn:
-                h = self.conv1(h)
+                h = compress_1x1(self.conv1, h)
             if self.opt.multi_gcn:
                 g.ndata["image"] = h
-                h = self.conv2(self.gcn2.forward_cat(g))  # models.py:186-189
+                h = compress_1x1(self.conv2, self.gcn2.forward_cat(g))  # models.py:186-189
             if not hasattr(self, "decoder"):
                 return h
             return self.decoder(h)
