@@ -151,6 +151,27 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride,
 int mrp_edge_hidden_fwd(const float* pose, const float* w1, const float* b1,
                         int32_t num_edges, int32_t C, float* h, void* stream);
 
+/*
+ * Per-frame robot graphs built on the device (dgl/dataloader.py:88-122 with the relative pose of
+ * dgl/utils.py:54-77), for a batch of num_graphs frames of n robots each (n <= MRP_MAX_NODES).
+ *
+ *   poses      (num_graphs * n, 7) fp32 rows (tx, ty, tz, qx, qy, qz, qw), graph by graph
+ *   knn_k      0: complete graphs, the reference topology: all ordered pairs u != v, edges numbered
+ *                 graph by graph i-major (the MRP_GRAPH_COMPLETE numbering), E = num_graphs*n*(n-1);
+ *              k (1 <= k < n): k-NN graphs: destination v's sources are the k robots u != v with the
+ *                 smallest |t_u - t_v| (float64, ties to the lower index), edges numbered
+ *                 destination-major with sources ascending, E = num_graphs*n*k (MRP_GRAPH_REGULAR(k))
+ *   edge_pose  (E, 9) fp32: cal_relative_pose(pose[src e], pose[dst e]), bit-identical to the
+ *              reference's float32 arithmetic
+ *   indptr     (num_graphs*n + 1), src (E), eid (E): CSR by destination, in-edges by increasing
+ *              edge id; graph_off (num_graphs + 1) — the graph arguments of the aggregation calls
+ * Any output pointer may be NULL to skip it.  Returns hipErrorInvalidValue for n > MRP_MAX_NODES,
+ * k >= n or sizes beyond int32.
+ */
+int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int32_t knn_k,
+                          float* edge_pose, int32_t* indptr, int32_t* src, int32_t* eid,
+                          int32_t* graph_off, void* stream);
+
 /* Library identification: ABI version (incremented on signature changes). */
 int mrp_abi_version(void);
 

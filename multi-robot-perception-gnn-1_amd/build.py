@@ -9,7 +9,12 @@ import sys
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
-SOURCES = [os.path.join(PKG_DIR, "csrc", "film_mean.hip"), os.path.join(PKG_DIR, "csrc", "edge_encoder.hip")]
+SOURCES = [os.path.join(PKG_DIR, "csrc", f) for f in ("film_mean_fwd.hip", "film_mean_bwd.hip", "film_mean_bwd_1_8.hip",
+                                                    "film_mean_bwd_9_12.hip", "film_mean_bwd_13_16.hip",
+                                                    "edge_encoder.hip", "frame_graph.hip")]
+OBJ_DIR = os.path.join(PKG_DIR, "build")
+HEADERS = [os.path.join(REPO, "include", "mrp_gnn.h")] + [os.path.join(PKG_DIR, "csrc", h) for h in (
+    "film_mean_kernels.hpp", "film_mean_bwd_launch.hpp")]
 OUT = os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
 ARCH = os.environ.get("MRP_OFFLOAD_ARCH", "gfx950")
 
@@ -25,17 +30,43 @@ def needs_build(out: str = OUT) -> bool:
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    deps = SOURCES + [os.path.join(REPO, "include", "mrp_gnn.h")]
+    deps = SOURCES + HEADERS
     return any(os.path.getmtime(s) > t for s in deps)
 
 
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mcode-object-version=5", "-ffp-contract=off", "-Wno-pass-failed"]
+
+
+def _compile(src: str, verbose: bool) -> str:
+    obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+    deps = [src] + HEADERS
+    if os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(d) for d in deps):
+        return obj
+    cmd = [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + ["-I", os.path.join(REPO, "include"), "-c", src,
+                                                      "-o", obj + ".tmp"]
+    if verbose:
+        print("[mrp_gnn build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(obj + ".tmp", obj)
+    return obj
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
+    """Compile every source to an object (in parallel, one hipcc per file) and link the library."""
     if not force and not needs_build():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    if force:
+        for src in SOURCES:
+            obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+            if os.path.exists(obj):
+                os.remove(obj)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), 8)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, verbose), SOURCES))
     tmp = OUT + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-mcode-object-version=5", "-ffp-contract=off",
-           "-Wno-pass-failed", "-I", os.path.join(REPO, "include"), "-o", tmp] + SOURCES
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print("[mrp_gnn build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -1,0 +1,74 @@
+// film_mean_bwd_launch.hpp — backward launch templates, included by the film_mean_bwd_*.hip parts.
+#pragma once
+#include "film_mean_kernels.hpp"
+
+namespace mrp_host {
+
+template <int NT, bool COMPLETE, bool DXB>
+hipError_t launch_bwd_ntb(const AggArgs& a_in, const Geometry& g, hipStream_t st) {
+  if constexpr (NT <= 8) {
+    const AggArgs& a = a_in;
+    const size_t lds = lds_bwd<NT>(g.cpb);
+    if (g.vec == 4)
+      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 4, COMPLETE, DXB>), lds);
+    else if (g.vec == 2)
+      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 2, COMPLETE, DXB>), lds);
+    else
+      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 1, COMPLETE, DXB>), lds);
+    return hipGetLastError();
+  } else {
+    if (a_in.want_dx) {
+      const AggArgs& a = a_in;
+      const size_t lds = lds_dx<NT>(g.cpb);
+      if (g.vec == 4)
+        MRP_LAUNCH((mrp::film_bwd_dx<NT, 4, COMPLETE, DXB>), lds);
+      else if (g.vec == 2)
+        MRP_LAUNCH((mrp::film_bwd_dx<NT, 2, COMPLETE, DXB>), lds);
+      else
+        MRP_LAUNCH((mrp::film_bwd_dx<NT, 1, COMPLETE, DXB>), lds);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    if (a_in.want_dgb) {
+      AggArgs a = a_in;
+      a.want_dx = 0;
+      const size_t lds = lds_bwd<NT>(g.cpb);
+      if (g.vec == 4)
+        MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 4, COMPLETE>), lds);
+      else if (g.vec == 2)
+        MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 2, COMPLETE>), lds);
+      else
+        MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 1, COMPLETE>), lds);
+      return hipGetLastError();
+    }
+    return hipSuccess;
+  }
+}
+
+template <int NT, int KMAX, bool DXB>
+hipError_t launch_bwd_regular(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  // VEC 4 would need 4*NT registers more per operand and spills; KMAX 8 only fits at VEC 1
+  const size_t lds = lds_regular<NT, KMAX>(g.cpb);
+  if constexpr (KMAX <= 4) {
+    if (g.vec == 2) {
+      MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 2, DXB>), lds);
+      return hipGetLastError();
+    }
+  }
+  MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 1, DXB>), lds);
+  return hipGetLastError();
+}
+
+template <int NT, bool COMPLETE>
+hipError_t launch_bwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  if constexpr (NT > 8 && !COMPLETE) {
+    // regular in-degree (k-NN): per-edge-slot Gram, one sweep
+    if (a.kdeg >= 1 && a.kdeg <= 4)
+      return a.dxb ? launch_bwd_regular<NT, 4, true>(a, g, st) : launch_bwd_regular<NT, 4, false>(a, g, st);
+    if (a.kdeg >= 5 && a.kdeg <= 8)
+      return a.dxb ? launch_bwd_regular<NT, 8, true>(a, g, st) : launch_bwd_regular<NT, 8, false>(a, g, st);
+  }
+  return a.dxb ? launch_bwd_ntb<NT, COMPLETE, true>(a, g, st) : launch_bwd_ntb<NT, COMPLETE, false>(a, g, st);
+}
+
+}  // namespace mrp_host

@@ -1,3 +1,4 @@
+#pragma once
 // film_mean.hip — gfx950 (MI355X / CDNA4) kernels for the FiLM-mean GCN aggregation.
 //
 // Hot path replaced (xjh19971/multi-robot-perception-gnn-1):
@@ -861,7 +862,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
 // ===========================================================================
 // Host side: validation, geometry, template dispatch, C ABI.
 // ===========================================================================
-namespace {
+namespace mrp_host {
 
 using mrp::AggArgs;
 
@@ -870,15 +871,15 @@ struct Geometry {
   int64_t grid;
 };
 
-bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+inline bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
 
 // Lanes per channel plane: the largest power of two <= clamp(P/vec/2, lo, hi) (two slices per lane
 // where the plane allows) and <= P/vec; channels per block fill the 256 threads up to max_cpb.
 // Measured optima (tools/kernel_lab.hip product sweep): forward lo=16, hi=64 (64 lanes at 32x32,
 // 32 at 16x16, 16 at 8x8); fused backward lo=8 (8 lanes x 32 channels at 8x8: 78 vs 87 us at
 // C=1280); regular backward 16.
-Geometry make_geometry(int C, int P, int vec, int lo, int hi, int max_cpb) {
+inline Geometry make_geometry(int C, int P, int vec, int lo, int hi, int max_cpb) {
   Geometry g;
   g.vec = vec;
   const int pv = P / g.vec;
@@ -917,86 +918,6 @@ size_t lds_bwd(int cpb) {
 
 #define MRP_LAUNCH(KERNEL, LDS) hipLaunchKernelGGL((KERNEL), dim3((unsigned)g.grid), dim3(g.threads), (LDS), st, a)
 
-template <int NT, bool COMPLETE>
-hipError_t launch_fwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
-  const size_t lds = lds_fwd<NT>(g.cpb);
-  if (g.vec == 4)
-    MRP_LAUNCH((mrp::film_fwd<NT, 4, COMPLETE>), lds);
-  else if (g.vec == 2)
-    MRP_LAUNCH((mrp::film_fwd<NT, 2, COMPLETE>), lds);
-  else if (g.vec == 1)
-    MRP_LAUNCH((mrp::film_fwd<NT, 1, COMPLETE>), lds);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
-template <int NT, bool COMPLETE, bool DXB>
-hipError_t launch_bwd_ntb(const AggArgs& a_in, const Geometry& g, hipStream_t st) {
-  if constexpr (NT <= 8) {
-    const AggArgs& a = a_in;
-    const size_t lds = lds_bwd<NT>(g.cpb);
-    if (g.vec == 4)
-      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 4, COMPLETE, DXB>), lds);
-    else if (g.vec == 2)
-      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 2, COMPLETE, DXB>), lds);
-    else
-      MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 1, COMPLETE, DXB>), lds);
-    return hipGetLastError();
-  } else {
-    if (a_in.want_dx) {
-      const AggArgs& a = a_in;
-      const size_t lds = lds_dx<NT>(g.cpb);
-      if (g.vec == 4)
-        MRP_LAUNCH((mrp::film_bwd_dx<NT, 4, COMPLETE, DXB>), lds);
-      else if (g.vec == 2)
-        MRP_LAUNCH((mrp::film_bwd_dx<NT, 2, COMPLETE, DXB>), lds);
-      else
-        MRP_LAUNCH((mrp::film_bwd_dx<NT, 1, COMPLETE, DXB>), lds);
-      hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
-    }
-    if (a_in.want_dgb) {
-      AggArgs a = a_in;
-      a.want_dx = 0;
-      const size_t lds = lds_bwd<NT>(g.cpb);
-      if (g.vec == 4)
-        MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 4, COMPLETE>), lds);
-      else if (g.vec == 2)
-        MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 2, COMPLETE>), lds);
-      else
-        MRP_LAUNCH((mrp::film_bwd_fused<NT, 4, 1, COMPLETE>), lds);
-      return hipGetLastError();
-    }
-    return hipSuccess;
-  }
-}
-
-template <int NT, int KMAX, bool DXB>
-hipError_t launch_bwd_regular(const AggArgs& a, const Geometry& g, hipStream_t st) {
-  // VEC 4 would need 4*NT registers more per operand and spills; KMAX 8 only fits at VEC 1
-  const size_t lds = lds_regular<NT, KMAX>(g.cpb);
-  if constexpr (KMAX <= 4) {
-    if (g.vec == 2) {
-      MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 2, DXB>), lds);
-      return hipGetLastError();
-    }
-  }
-  MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 1, DXB>), lds);
-  return hipGetLastError();
-}
-
-template <int NT, bool COMPLETE>
-hipError_t launch_bwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
-  if constexpr (NT > 8 && !COMPLETE) {
-    // regular in-degree (k-NN): per-edge-slot Gram, one sweep
-    if (a.kdeg >= 1 && a.kdeg <= 4)
-      return a.dxb ? launch_bwd_regular<NT, 4, true>(a, g, st) : launch_bwd_regular<NT, 4, false>(a, g, st);
-    if (a.kdeg >= 5 && a.kdeg <= 8)
-      return a.dxb ? launch_bwd_regular<NT, 8, true>(a, g, st) : launch_bwd_regular<NT, 8, false>(a, g, st);
-  }
-  return a.dxb ? launch_bwd_ntb<NT, COMPLETE, true>(a, g, st) : launch_bwd_ntb<NT, COMPLETE, false>(a, g, st);
-}
 
 #define MRP_DISPATCH_NT(NTV, COMPLETE, FN, ...)                                        \
   switch (NTV) {                                                                       \
@@ -1019,14 +940,8 @@ hipError_t launch_bwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
     default: return hipErrorInvalidValue;                                              \
   }
 
-hipError_t dispatch_fwd(int nt, bool complete, const AggArgs& a, const Geometry& g, hipStream_t st) {
-  MRP_DISPATCH_NT(nt, complete, launch_fwd_nt, a, g, st)
-}
-hipError_t dispatch_bwd(int nt, bool complete, const AggArgs& a, const Geometry& g, hipStream_t st) {
-  MRP_DISPATCH_NT(nt, complete, launch_bwd_nt, a, g, st)
-}
 
-bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* eid, const int32_t* graph_off,
+inline bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* eid, const int32_t* graph_off,
                     int32_t num_graphs, int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges,
                     int32_t C, int32_t P, int32_t mode) {
   if (num_graphs < 0 || num_nodes < 0 || num_edges < 0 || C < 0 || P < 0) return false;
@@ -1049,162 +964,17 @@ bool common_args_ok(const int32_t* indptr, const int32_t* src, const int32_t* ei
   return true;
 }
 
-}  // namespace
 
-extern "C" {
+}  // namespace mrp_host
 
-int mrp_abi_version(void) { return 7; }
+// One case of a switch over the compile-time maximum graph size.
+#define MRP_NT_CASE(N, COMPLETE, FN, ...) \
+  case N: return COMPLETE ? FN<N, true>(__VA_ARGS__) : FN<N, false>(__VA_ARGS__);
 
-const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
+namespace mrp_host {
+// backward dispatch, split over translation units by graph size (they compile in parallel)
+hipError_t dispatch_bwd_1_8(int nt, bool complete, const AggArgs& a, const Geometry& g, hipStream_t st);
+hipError_t dispatch_bwd_9_12(int nt, bool complete, const AggArgs& a, const Geometry& g, hipStream_t st);
+hipError_t dispatch_bwd_13_16(int nt, bool complete, const AggArgs& a, const Geometry& g, hipStream_t st);
+}  // namespace mrp_host
 
-}  // extern "C"
-
-namespace {
-
-int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr, const int32_t* src,
-                  const int32_t* eid, const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes,
-                  int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode_flags,
-                  float* out, int64_t out_node_stride, float* xcopy, int64_t xcopy_node_stride, void* stream) {
-  const int32_t logits = (mode_flags & MRP_AGG_GB_LOGITS) ? 1 : 0;
-  const int32_t mode = mode_flags & ~MRP_AGG_GB_LOGITS;
-  if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind, num_nodes, num_edges, C, P,
-                      mode))
-    return hipErrorInvalidValue;
-  if (num_graphs == 0 || num_nodes == 0 || max_nodes == 0 || C == 0 || P == 0) return hipSuccess;
-  const int64_t plane = (int64_t)C * P;
-  if (x == nullptr || out == nullptr || x_node_stride < plane || out_node_stride < plane)
-    return hipErrorInvalidValue;
-  if (mode != MRP_AGG_COPY_MEAN && num_edges > 0 && gb == nullptr) return hipErrorInvalidValue;
-  if (xcopy != nullptr && xcopy_node_stride < plane) return hipErrorInvalidValue;
-  bool vec4 =
-      (P % 4 == 0) && (x_node_stride % 4 == 0) && (out_node_stride % 4 == 0) && aligned16(x) && aligned16(out);
-  if (xcopy != nullptr) vec4 = vec4 && (xcopy_node_stride % 4 == 0) && aligned16(xcopy);
-  // 16-byte slices beat 8-byte ones at every measured size (tools/kernel_lab.hip product sweep)
-  Geometry g = make_geometry(C, P, vec4 ? 4 : 1, 16, 64, mrp::kMaxChanPerBlock);
-  g.grid = (int64_t)num_graphs * g.ncb;
-  if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
-  AggArgs a = {};
-  a.x = x;
-  a.xs = x_node_stride;
-  a.gb = gb;
-  a.indptr = indptr;
-  a.src = src;
-  a.eid = eid;
-  a.goff = graph_off;
-  a.out = out;
-  a.os = out_node_stride;
-  a.C = C;
-  a.P = P;
-  a.PV = P / g.vec;
-  a.mode = mode;
-  a.lpc = g.lpc;
-  a.cpb = g.cpb;
-  a.ncb = g.ncb;
-  a.logits = logits;
-  a.xc = xcopy;
-  a.xcs = xcopy_node_stride;
-  return dispatch_fwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, static_cast<hipStream_t>(stream));
-}
-
-}  // namespace
-
-extern "C" {
-
-int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr,
-                      const int32_t* src, const int32_t* eid, const int32_t* graph_off, int32_t num_graphs,
-                      int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C,
-                      int32_t P, int32_t mode_flags, float* out, int64_t out_node_stride, void* stream) {
-  return film_fwd_impl(x, x_node_stride, gb, indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind,
-                       num_nodes, num_edges, C, P, mode_flags, out, out_node_stride, nullptr, 0, stream);
-}
-
-int mrp_film_mean_cat_fwd(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr,
-                          const int32_t* src, const int32_t* eid, const int32_t* graph_off, int32_t num_graphs,
-                          int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C,
-                          int32_t P, int32_t mode_flags, float* cat, int64_t cat_node_stride, void* stream) {
-  if (cat == nullptr || cat_node_stride < 2 * (int64_t)C * P) return hipErrorInvalidValue;
-  return film_fwd_impl(x, x_node_stride, gb, indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind,
-                       num_nodes, num_edges, C, P, mode_flags, cat + (int64_t)C * P, cat_node_stride, cat,
-                       cat_node_stride, stream);
-}
-
-int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float* x, int64_t x_node_stride,
-                      const float* gb, const int32_t* indptr, const int32_t* src, const int32_t* eid,
-                      const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
-                      int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode_flags, float* grad_x,
-                      int64_t gx_node_stride, const float* grad_x_base, int64_t base_node_stride, float* grad_gb,
-                      void* stream) {
-  const int32_t logits = (mode_flags & MRP_AGG_GB_LOGITS) ? 1 : 0;
-  const int32_t mode = mode_flags & ~MRP_AGG_GB_LOGITS;
-  if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind, num_nodes, num_edges, C, P,
-                      mode))
-    return hipErrorInvalidValue;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const bool copy = mode == MRP_AGG_COPY_MEAN;
-  if (grad_gb != nullptr && num_edges > 0 && C > 0 && (copy || num_nodes == 0 || P == 0)) {
-    // gamma/beta do not influence the output: their gradient is zero.
-    hipError_t e = hipMemsetAsync(grad_gb, 0, (size_t)num_edges * C * 2 * sizeof(float), st);
-    if (e != hipSuccess) return e;
-  }
-  const bool want_dgb = grad_gb != nullptr && !copy && num_edges > 0;
-  const bool want_dx = grad_x != nullptr;
-  if (!want_dgb && !want_dx) return hipSuccess;
-  if (num_graphs == 0 || num_nodes == 0 || max_nodes == 0 || C == 0 || P == 0) return hipSuccess;
-  const int64_t plane = (int64_t)C * P;
-  if (grad_out == nullptr || g_node_stride < plane) return hipErrorInvalidValue;
-  if (want_dx && gx_node_stride < plane) return hipErrorInvalidValue;
-  if (want_dx && grad_x_base != nullptr && base_node_stride < plane) return hipErrorInvalidValue;
-  if (want_dgb && (x == nullptr || x_node_stride < plane)) return hipErrorInvalidValue;
-  if (!copy && num_edges > 0 && gb == nullptr) return hipErrorInvalidValue;
-  bool vec4 = (P % 4 == 0) && (g_node_stride % 4 == 0) && aligned16(grad_out);
-  if (want_dx) vec4 = vec4 && (gx_node_stride % 4 == 0) && aligned16(grad_x);
-  if (want_dx && grad_x_base) vec4 = vec4 && (base_node_stride % 4 == 0) && aligned16(grad_x_base);
-  if (want_dgb) vec4 = vec4 && (x_node_stride % 4 == 0) && aligned16(x);
-  // 16-byte slices: with the DPP lane reduction they beat 8-byte slices (310 vs 322 us at B=32,
-  // N=8, C=512, 32x32) despite 2 waves/SIMD instead of 3.  VEC=2 stays compiled for experiments.
-  int vec = vec4 ? 4 : 1;
-  Geometry g;
-  const int kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
-  if (max_nodes > 8 && kdeg >= 1 && kdeg <= 8) {
-    // film_bwd_regular: 8-byte slices on 16 lanes per plane (367 us against 569 us on 64 lanes at
-    // k-NN(4) N=16 C=1024 16x16): its prologue and lane reduction are amortised over more slices
-    vec = (vec4 && kdeg <= 4) ? 2 : 1;
-    g = vec == 2 ? make_geometry(C, P, 2, 16, 16, mrp::kMaxChanPerBlock)
-                 : make_geometry(C, P, 1, 32, 32, mrp::kMaxChanPerBlock);
-  } else if (max_nodes <= 8) {
-    g = make_geometry(C, P, vec, 8, 64, 32);  // film_bwd_fused
-  } else {
-    g = make_geometry(C, P, vec, 64, 64, mrp::kMaxChanPerBlock);  // film_bwd_dx + Gram pass
-  }
-  g.grid = (int64_t)num_graphs * g.ncb;
-  if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
-  AggArgs a = {};
-  a.x = x;
-  a.xs = x_node_stride;
-  a.g = grad_out;
-  a.gs = g_node_stride;
-  a.gb = gb;
-  a.indptr = indptr;
-  a.src = src;
-  a.eid = eid;
-  a.goff = graph_off;
-  a.out = grad_x;
-  a.os = gx_node_stride;
-  a.dgb = grad_gb;
-  a.C = C;
-  a.P = P;
-  a.PV = P / g.vec;
-  a.mode = mode;
-  a.lpc = g.lpc;
-  a.cpb = g.cpb;
-  a.ncb = g.ncb;
-  a.want_dx = want_dx ? 1 : 0;
-  a.want_dgb = want_dgb ? 1 : 0;
-  a.logits = logits;
-  a.dxb = want_dx ? grad_x_base : nullptr;
-  a.dxbs = base_node_stride;
-  a.kdeg = kdeg;
-  return dispatch_bwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, st);
-}
-
-}  // extern "C"

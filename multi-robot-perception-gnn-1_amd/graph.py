@@ -81,8 +81,9 @@ class RobotGraph:
         n = inferred if num_nodes is None else int(num_nodes)
         if n < inferred:
             raise ValueError(f"num_nodes={n} but edges reference node {inferred - 1}")
-        self._src = src_t
-        self._dst = dst_t
+        self._edge_store = (src_t, dst_t)
+        self._edge_fn = None
+        self._ne = int(src_t.numel())
         self._num_nodes = n
         self._bnn = [n] if batch_num_nodes is None else [int(v) for v in batch_num_nodes]
         self._bne = [src_t.numel()] if batch_num_edges is None else [int(v) for v in batch_num_edges]
@@ -93,12 +94,49 @@ class RobotGraph:
         self._csr_cache: Dict[str, GraphCSR] = {}
         self._host_csr = None
 
+    @classmethod
+    def _from_device(cls, edge_fn, num_nodes: int, num_edges: int, bnn: Sequence[int], bne: Sequence[int],
+                     csr: Optional[GraphCSR] = None, device=None, complete: Optional[bool] = None,
+                     kdeg: Optional[int] = None) -> "RobotGraph":
+        """A graph whose structure was built on the device (``frame_batch``): the host edge list is
+        produced by ``edge_fn()`` only if something asks for it (``edges()``, ``host_csr()``)."""
+        g = cls.__new__(cls)
+        g._edge_store = None
+        g._edge_fn = edge_fn
+        g._ne = int(num_edges)
+        g._num_nodes = int(num_nodes)
+        g._bnn, g._bne = [int(v) for v in bnn], [int(v) for v in bne]
+        g.ndata = _FeatureDict(g._num_nodes, "ndata")
+        g.edata = _FeatureDict(g._ne, "edata")
+        g._csr_cache = {}
+        if csr is not None:
+            g._csr_cache[(str(torch.device(device)), csr.graph_kind)] = csr
+        g._host_csr = None
+        g._complete = complete
+        g._kdeg = kdeg
+        return g
+
+    @property
+    def _src(self) -> torch.Tensor:
+        return self._edges_host()[0]
+
+    @property
+    def _dst(self) -> torch.Tensor:
+        return self._edges_host()[1]
+
+    def _edges_host(self):
+        if self._edge_store is None:
+            src, dst = self._edge_fn()
+            self._edge_store = (torch.as_tensor(src, dtype=torch.int64).cpu(),
+                                torch.as_tensor(dst, dtype=torch.int64).cpu())
+        return self._edge_store
+
     # ----------------------------------------------------------------- DGL-like API
     def num_nodes(self) -> int:
         return self._num_nodes
 
     def num_edges(self) -> int:
-        return int(self._src.numel())
+        return self._ne
 
     @property
     def batch_size(self) -> int:
@@ -140,7 +178,8 @@ class RobotGraph:
     def to(self, device, non_blocking: bool = False) -> "RobotGraph":
         """A graph sharing this structure with every feature moved to ``device``."""
         g = RobotGraph.__new__(RobotGraph)
-        g._src, g._dst, g._num_nodes = self._src, self._dst, self._num_nodes
+        # share the structure (and its lazily built host edge list) without materialising it
+        g._edge_store, g._edge_fn, g._ne, g._num_nodes = self._edge_store, self._edge_fn, self._ne, self._num_nodes
         g._bnn, g._bne = list(self._bnn), list(self._bne)
         g.ndata = _FeatureDict(self._num_nodes, "ndata")
         g.edata = _FeatureDict(self.num_edges(), "edata")

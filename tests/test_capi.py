@@ -85,3 +85,18 @@ def test_no_cpu_fallback():
     x = torch.randn(3, 2, 4, 4)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         m.film_mean(x, torch.rand(6, 2, 2), g.csr("cpu"))
+
+
+def test_frame_graph_build_validation_without_launch():
+    lib = m.load_library()
+    dummy = ctypes.c_void_p(16)
+    # more robots per frame than MRP_MAX_NODES, k >= n, negative sizes: rejected before any launch
+    assert lib.mrp_frame_graph_build(dummy, 1, 17, 0, dummy, dummy, dummy, dummy, dummy, None) == HIP_INVALID_VALUE
+    assert lib.mrp_frame_graph_build(dummy, 1, 4, 4, dummy, dummy, dummy, dummy, dummy, None) == HIP_INVALID_VALUE
+    assert lib.mrp_frame_graph_build(dummy, -1, 4, 0, dummy, dummy, dummy, dummy, dummy, None) == HIP_INVALID_VALUE
+    assert lib.mrp_frame_graph_build(None, 2, 4, 0, None, None, None, None, None, None) == HIP_INVALID_VALUE
+
+
+def test_frame_batch_needs_the_gpu():
+    with pytest.raises(RuntimeError, match="GPU"):
+        m.frame_batch(torch.zeros(2, 4, 7))

@@ -6,7 +6,11 @@
 //   plane_copy<N> : the product's lane mapping with out_v = x_v (no prologue, no math)
 //   film_fwd<N,4> : the product kernel at several (lanes-per-channel, channels-per-block) geometries
 // Usage: kernel_lab [B N C HW iters]
-#include "../multi-robot-perception-gnn-1_amd/csrc/film_mean.hip"
+#include "../multi-robot-perception-gnn-1_amd/csrc/film_mean_fwd.hip"
+#include "../multi-robot-perception-gnn-1_amd/csrc/film_mean_bwd.hip"
+#include "../multi-robot-perception-gnn-1_amd/csrc/film_mean_bwd_1_8.hip"
+#include "../multi-robot-perception-gnn-1_amd/csrc/film_mean_bwd_9_12.hip"
+#include "../multi-robot-perception-gnn-1_amd/csrc/film_mean_bwd_13_16.hip"
 
 
 #include <algorithm>
