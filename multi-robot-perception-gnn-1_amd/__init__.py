@@ -9,7 +9,7 @@ name is not a Python identifier).
 from ._lib import MAX_NODES, MAX_REGULAR_K, MODES, graph_regular, load_library  # noqa: F401
 from .aggregate import (FilmMeanFunction, film_mean, film_mean_cat, film_mean_cat_forward_into,  # noqa: F401
                         film_mean_forward_into)
-from . import compress, encoder  # noqa: F401
+from . import compat, compress, encoder  # noqa: F401
 from .device_graph import frame_batch  # noqa: F401
 from .graph import (GraphCSR, RobotGraph, batch, complete_edges, complete_graph, frame_graph,  # noqa: F401
                     graph, knn_edges)

@@ -1,0 +1,113 @@
+"""Drop-in compatibility with the reference harness (``dgl/training.py``, ``dgl/eval.py``).
+
+The reference harness touches this path through two imports and one file format:
+
+* ``from model import models`` (``dgl/training.py:13``) and ``models.multi_view_dgl_model(opt)``
+  (``:303-304``); checkpoints are whole pickled modules, ``torch.save({'model': model, ...})``
+  (``dgl/training.py:339-355``), reloaded with ``checkpoint['model']`` (``dgl/training.py:289-291``,
+  ``dgl/eval.py:251-252``).  Unpickling resolves classes by their path ``model.models.<name>``.
+* ``from dgl import batch`` as the DataLoader collate (``dgl/training.py:15,57-58``,
+  ``dgl/eval.py:12,55-56``) and ``data.to('cuda:0')`` on its result.
+
+:func:`install` registers two import aliases so that both work on top of this package:
+
+* ``model.models`` — ``GCN``, ``edge_encoder`` and ``multi_view_dgl_model`` resolve to the
+  MI355X classes (identical attribute names and ``state_dict`` keys, so a reference checkpoint
+  unpickles straight into them); every other name (the torchvision ``encoder``, ``decoder``,
+  ``TransBlock``, the non-graph baselines — outside the hot path) is looked up in ``fallback``,
+  the caller's own import of the reference ``models`` module, if one is given.
+* ``dgl`` (only when the real DGL is not importable) — ``batch``, ``graph`` and ``DGLGraph``
+  backed by :class:`~graph.RobotGraph`.
+
+With the aliases installed, the reference's own ``train_dgl``/``test_dgl`` loops run unchanged:
+the collate yields a :class:`~graph.RobotGraph`, ``.to('cuda:0')`` moves its features, and the
+model's GCN layers run the HIP kernels.  Loading pickles executes code from the file: only load
+checkpoints you trust (``torch.load(..., weights_only=False)``); for untrusted files use
+``state_dict`` loading — the keys are identical (``tests/test_compat.py``).
+"""
+from __future__ import annotations
+
+import contextlib
+import importlib.util
+import sys
+import types
+from typing import Optional
+
+from . import graph as _graph
+from . import models as _models
+
+#: names the aliased ``model.models`` serves from this package
+NATIVE_CLASSES = ("GCN", "edge_encoder", "multi_view_dgl_model")
+
+
+def collate(graphs):
+    """The harness's ``_collate_fn`` (``dgl/training.py:57-58``): ``dgl.batch`` of frame graphs."""
+    return _graph.batch(graphs)
+
+
+def models_module(fallback: Optional[types.ModuleType] = None) -> types.ModuleType:
+    """A module object standing in for the reference's ``model.models``."""
+    mod = types.ModuleType("model.models")
+    mod.__doc__ = "mrp_gnn_amd alias of the reference's dgl/model/models.py (hot-path classes native)"
+    for name in NATIVE_CLASSES:
+        setattr(mod, name, getattr(_models, name))
+
+    def __getattr__(name):  # PEP 562: reference-only classes come from the caller's fallback
+        if fallback is not None and hasattr(fallback, name):
+            return getattr(fallback, name)
+        raise AttributeError(
+            f"model.models.{name} is outside the MI355X hot path; pass the reference module as "
+            f"install(fallback=...) to resolve it")
+
+    mod.__getattr__ = __getattr__
+    return mod
+
+
+def dgl_module() -> types.ModuleType:
+    """The slice of the ``dgl`` namespace the harness imports on this path."""
+    mod = types.ModuleType("dgl")
+    mod.__doc__ = "mrp_gnn_amd stand-in for dgl (batch / graph / DGLGraph on RobotGraph)"
+    mod.batch = _graph.batch
+    mod.graph = _graph.graph
+    mod.DGLGraph = _graph.RobotGraph
+    return mod
+
+
+def _dgl_importable() -> bool:
+    mod = sys.modules.get("dgl")
+    if mod is not None:
+        return not getattr(mod, "__doc__", "").startswith("mrp_gnn_amd")
+    return importlib.util.find_spec("dgl") is not None
+
+
+def install(fallback: Optional[types.ModuleType] = None, dgl: bool = True) -> dict:
+    """Register the ``model.models`` (and, if DGL is absent, ``dgl``) aliases in ``sys.modules``.
+    Returns the previous entries, for :func:`uninstall`."""
+    saved = {k: sys.modules.get(k) for k in ("model", "model.models", "dgl")}
+    pkg = types.ModuleType("model")
+    pkg.__path__ = []  # a package, so ``from model import models`` and pickle's import both work
+    pkg.models = models_module(fallback)
+    sys.modules["model"] = pkg
+    sys.modules["model.models"] = pkg.models
+    if dgl and not _dgl_importable():
+        sys.modules["dgl"] = dgl_module()
+    return saved
+
+
+def uninstall(saved: dict) -> None:
+    for k, v in saved.items():
+        if v is None:
+            sys.modules.pop(k, None)
+        else:
+            sys.modules[k] = v
+
+
+@contextlib.contextmanager
+def reference_class_path(fallback: Optional[types.ModuleType] = None, dgl: bool = True):
+    """``with reference_class_path(): ckpt = torch.load(path, weights_only=False)`` — unpickle a
+    reference checkpoint into the MI355X classes."""
+    saved = install(fallback, dgl)
+    try:
+        yield sys.modules["model.models"]
+    finally:
+        uninstall(saved)

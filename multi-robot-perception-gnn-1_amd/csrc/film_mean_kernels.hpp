@@ -264,7 +264,8 @@ __device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, 
 }
 
 template <int NT, bool BWD>
-__device__ __forceinline__ void complete_store(const AggArgs& a, int base, const float2* reg, float* Ga, float* Gb) {
+__device__ __forceinline__ void complete_store(const AggArgs& a, int base, const float2* reg, float* Ga, float* Gb,
+                                               float2* Sg = nullptr) {
   constexpr int S = CompleteSlots<NT>::kSlots;
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
@@ -279,6 +280,7 @@ __device__ __forceinline__ void complete_store(const AggArgs& a, int base, const
       const int v = slot / NT, u = slot - v * NT;
       if (BWD) {
         Ga[cl * SZ + u * NTP + v] = s * reg[r].x;
+        if (Sg != nullptr) Sg[t] = reg[r];  // sigmoid(z) of slot (cl, v, u), reused by the epilogue
       } else {
         Ga[cl * SZ + v * NTP + u] = reg[r].x;
         Gb[cl * SZ + v * NTP + u] = reg[r].y;
@@ -289,12 +291,13 @@ __device__ __forceinline__ void complete_store(const AggArgs& a, int base, const
 
 // Remaining slot chunks (only when a small workgroup owns more than kPer slots per thread).
 template <int NT, bool BWD>
-__device__ __forceinline__ void complete_rest(const AggArgs& a, int64_t ebase, int c0, float* Ga, float* Gb) {
+__device__ __forceinline__ void complete_rest(const AggArgs& a, int64_t ebase, int c0, float* Ga, float* Gb,
+                                              float2* Sg = nullptr) {
   const int chunk = CompleteSlots<NT>::kPer * blockDim.x;
   for (int base = chunk; base < a.cpb * CompleteSlots<NT>::kSlots; base += chunk) {
     float2 reg[CompleteSlots<NT>::kPer];
     complete_fetch<NT>(a, ebase, c0, base, reg);
-    complete_store<NT, BWD>(a, base, reg, Ga, Gb);
+    complete_store<NT, BWD>(a, base, reg, Ga, Gb, Sg);
   }
 }
 
@@ -529,6 +532,9 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   float* Dl = Wt + a.cpb * SZ;   // [cpb][NT][NTP]   Gram (unscaled)
   float* Sl = Dl + a.cpb * SZ;   // [cpb][NTP]       sum_p G_v
   float* sc = Sl + a.cpb * NTP;  // [NTP]            s_v
+  // COMPLETE with logits: sigmoid(z) of every slot, (cpb x NT x NT) float2 in complete_fetch order,
+  // so the epilogue's sigmoid backward does not fetch z from HBM a second time
+  float2* Sg = (COMPLETE && a.logits) ? reinterpret_cast<float2*>(sc + NTP) : nullptr;
 
   const int b = blockIdx.x / a.ncb;
   const int cb = blockIdx.x - b * a.ncb;
@@ -536,16 +542,6 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   const int n = COMPLETE ? NT : min(a.goff[b + 1] - node0, NT);
   if (n <= 0) return;
   const int c0 = cb * a.cpb;
-
-  if (COMPLETE) {
-    float2 reg[CompleteSlots<NT>::kPer];
-    complete_fetch<NT>(a, (int64_t)b * NT * (NT - 1), c0, 0, reg);
-    complete_store<NT, true>(a, 0, reg, Wt, nullptr);
-    complete_rest<NT, true>(a, (int64_t)b * NT * (NT - 1), c0, Wt, nullptr);
-  } else {
-    build_tiles_csr<NT, true>(a, node0, n, c0, Wt, nullptr, sc, nullptr);
-  }
-  __syncthreads();
 
   const int grp = threadIdx.x / a.lpc;
   const int li = threadIdx.x - grp * a.lpc;
@@ -556,6 +552,38 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   const float* xbase = a.x + (int64_t)node0 * a.xs + (int64_t)c * a.P;
   float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
   const bool do_dx = kOnePass && a.want_dx;
+
+  // slice fragments: for the one-pass kernel the first slice is loaded before the prologue, so the
+  // weight-tile build (one more round trip to HBM) hides under these loads
+  Frag<VEC> gv[VB];
+  Frag<VEC> xv[NT];
+  auto load_slice = [&](int vb, int j) {
+    const int64_t off = (int64_t)j * VEC;
+#pragma unroll
+    for (int i = 0; i < VB; ++i) {
+      const int v = vb + i;
+      const int vv = v < n ? v : n - 1;
+      gv[i] = load_frag<VEC, kOnePass>(gbase + (int64_t)vv * a.gs + off);
+    }
+    if (a.want_dgb) {
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        const int uu = u < n ? u : n - 1;
+        xv[u] = load_frag<VEC, kOnePass>(xbase + (int64_t)uu * a.xs + off);
+      }
+    }
+  };
+
+  float2 reg[CompleteSlots<NT>::kPer];
+  if (COMPLETE) complete_fetch<NT>(a, (int64_t)b * NT * (NT - 1), c0, 0, reg);
+  if (kOnePass && active && li < a.PV) load_slice(0, li);
+  if (COMPLETE) {
+    complete_store<NT, true>(a, 0, reg, Wt, nullptr, Sg);
+    complete_rest<NT, true>(a, (int64_t)b * NT * (NT - 1), c0, Wt, nullptr, Sg);
+  } else {
+    build_tiles_csr<NT, true>(a, node0, n, c0, Wt, nullptr, sc, nullptr);
+  }
+  __syncthreads();
 
 #pragma unroll 1
   for (int vb = 0; vb < NT; vb += VB) {
@@ -568,26 +596,13 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
       for (int u = 0; u < NT; ++u) D[i][u] = 0.f;
     }
     if (active) {
-      for (int j = li; j < a.PV; j += a.lpc) {
+      int j = li;
+      if (!kOnePass && j < a.PV) load_slice(vb, j);
+      while (j < a.PV) {
         const int64_t off = (int64_t)j * VEC;
         int tile = grp * SZ;  // laundered: keep the weights in LDS, not hoisted into registers
         asm volatile("" : "+v"(tile));
         const float* W = Wt + tile;
-        Frag<VEC> gv[VB];
-        Frag<VEC> xv[NT];
-#pragma unroll
-        for (int i = 0; i < VB; ++i) {
-          const int v = vb + i;
-          const int vv = v < n ? v : n - 1;
-          gv[i] = load_frag<VEC, kOnePass>(gbase + (int64_t)vv * a.gs + off);
-        }
-        if (a.want_dgb) {
-#pragma unroll
-          for (int u = 0; u < NT; ++u) {
-            const int uu = u < n ? u : n - 1;
-            xv[u] = load_frag<VEC, kOnePass>(xbase + (int64_t)uu * a.xs + off);
-          }
-        }
         if (do_dx) {
 #pragma unroll
           for (int u = 0; u < NT; ++u) {
@@ -627,6 +642,8 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
             }
           }
         }
+        j += a.lpc;
+        if (j < a.PV) load_slice(vb, j);
       }
     }
     if (a.want_dgb) {
@@ -668,7 +685,11 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
       if (u == v || cc >= a.C) continue;
       float2 r = make_float2(s * Dl[cl * SZ + v * NTP + u], s * Sl[cl * NTP + v]);
       const int64_t off = (complete_eid(ebase, NT, u, v) * a.C + cc) * 2;
-      if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
+      if (a.logits) {
+        // d z = d(gamma, beta) * sig * (1 - sig), sig = sigmoid(z) kept from the prologue
+        const float2 sg = Sg[t];
+        r = make_float2(r.x * sg.x * (1.f - sg.x), r.y * sg.y * (1.f - sg.y));
+      }
       *reinterpret_cast<float2*>(a.dgb + off) = r;
     }
     return;
@@ -912,8 +933,10 @@ size_t lds_regular(int cpb) {
          2 * (size_t)NT * KMAX * sizeof(int);
 }
 template <int NT>
-size_t lds_bwd(int cpb) {
-  return (size_t)(2 * cpb * mrp::Tile<NT>::SZ + cpb * mrp::Tile<NT>::NTP + mrp::Tile<NT>::NTP) * sizeof(float);
+size_t lds_bwd(int cpb, bool complete_logits) {
+  // + the per-slot sigmoid values (float2) the COMPLETE epilogue reuses
+  return (size_t)(2 * cpb * mrp::Tile<NT>::SZ + cpb * mrp::Tile<NT>::NTP + mrp::Tile<NT>::NTP) * sizeof(float) +
+         (complete_logits ? (size_t)cpb * NT * NT * sizeof(float2) : 0);
 }
 
 #define MRP_LAUNCH(KERNEL, LDS) hipLaunchKernelGGL((KERNEL), dim3((unsigned)g.grid), dim3(g.threads), (LDS), st, a)

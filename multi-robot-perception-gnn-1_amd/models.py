@@ -149,18 +149,33 @@ class multi_view_dgl_model(nn.Module):  # noqa: N801  (reference class name)
             self.gcn2 = GCN(opt)
             self.conv2 = nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1)
 
-    def features(self, g) -> torch.Tensor:
-        """Encoder output per node, (B*N, C, h, w) (``models.py:175-179``)."""
+    def features(self, g):
+        """Encoder output per node, (B*N, C, h, w), and the encoder's feature list
+        (``models.py:175-179``)."""
         image = g.ndata["image"]
         if not hasattr(self, "encoder"):
-            return image
+            return image, [image]
         image = image.view(-1, self.opt.camera_num, 3, self.opt.image_size, self.opt.image_size)
-        h = self.encoder(image)[-1]
-        return h.view(-1, h.size()[-3], h.size()[-2], h.size()[-1])
+        h_list = self.encoder(image)
+        h = h_list[-1]
+        return h.view(-1, h.size()[-3], h.size()[-2], h.size()[-1]), h_list
+
+    def decode(self, h, h_list):
+        """The decoder heads of ``models.py:190-205``: ``skip_level`` also passes the encoder's
+        feature list; ``task='depthseg'`` calls ``depth_decoder`` and ``seg_decoder``."""
+        if _opt(self.opt, "task", "depth") == "depthseg" and hasattr(self, "depth_decoder"):
+            heads = (self.depth_decoder, self.seg_decoder)
+        elif hasattr(self, "decoder"):
+            heads = (self.decoder,)
+        else:
+            return h  # no decoder supplied: the GCN block's output (the benchmark setting)
+        args = (h, h_list) if _opt(self.opt, "skip_level", False) else (h,)
+        outs = tuple(head(*args) for head in heads)
+        return outs if len(outs) > 1 else outs[0]
 
     def forward(self, g):
         with g.local_scope():
-            h = self.features(g)
+            h, h_list = self.features(g)
             g.ndata["image"] = h
             h = self.gcn1.forward_cat(g)  # cat((h, gcn1(g)), 1), models.py:181-182
             if self.opt.compress_gcn:
@@ -168,6 +183,4 @@ class multi_view_dgl_model(nn.Module):  # noqa: N801  (reference class name)
             if self.opt.multi_gcn:
                 g.ndata["image"] = h
                 h = compress_1x1(self.conv2, self.gcn2.forward_cat(g))  # models.py:186-189
-            if not hasattr(self, "decoder"):
-                return h
-            return self.decoder(h)
+            return self.decode(h, h_list)

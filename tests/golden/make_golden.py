@@ -185,8 +185,56 @@ def make_case(models, utils, name, graphs, C, H, W, seed, mode="film_mean"):
           f"-> {os.path.getsize(path)} B")
 
 
+def make_checkpoint(models, utils, seed=11):
+    """A checkpoint in the reference harness's format (``torch.save({'model': module, ...})``,
+    dgl/training.py:350-353) holding reference ``GCN`` modules (class path ``model.models.GCN``),
+    plus the reference's aggregate for a small complete batch computed with them.  Loaded by
+    tests/test_compat.py through the ``model.models`` alias (mrp_gnn_amd.compat)."""
+    import argparse
+    torch.manual_seed(seed)
+    C, H, W, n = 8, 4, 4, 4
+    opt = argparse.Namespace(feature_dim=C, compress_gcn=True, multi_gcn=True, camera_num=n, image_size=128,
+                             skip_level=False, task="depth")
+    holder = torch.nn.Module()  # stands in for multi_view_dgl_model's GCN part (its encoder needs torchvision)
+    holder.gcn1 = models.GCN(opt)
+    holder.conv1 = torch.nn.Conv2d(2 * C, C, kernel_size=1)
+    holder.gcn2 = models.GCN(opt)
+    holder.conv2 = torch.nn.Conv2d(2 * C, C, kernel_size=1)
+    rng = np.random.RandomState(seed)
+    graphs = []
+    for _ in range(2):
+        p = random_poses(rng, n)
+        graphs.append((n, *complete_edges(n), p))
+    src, dst, pose = [], [], []
+    for b, (nn_, s, d, p) in enumerate(graphs):
+        src += [u + b * n for u in s]
+        dst += [v + b * n for v in d]
+        pose += [utils.cal_relative_pose(p[u], p[v]) for u, v in zip(s, d)]
+    pose = torch.from_numpy(np.stack(pose)).float()
+    x = torch.randn(2 * n, C, H, W)
+    with torch.no_grad():
+        outs = []
+        for gcn in (holder.gcn1, holder.gcn2):
+            g = DGLGraphShim(src, dst, 2 * n)
+            g.ndata["image"] = x
+            g.edata["pose"] = pose
+            g.edata["pose_gamma"], g.edata["pose_beta"] = gcn.edge_encoder(pose)
+            g.update_all(models.edge_udf, models.node_udf)
+            outs.append(g.ndata["images"])
+    path = os.path.join(OUT_DIR, "ref_gcn_checkpoint.pt")
+    torch.save({"model": holder.gcn1, "stack": holder, "n_iter": 3}, path)
+    np.savez_compressed(os.path.join(OUT_DIR, "ref_gcn_checkpoint_io.npz"), x=x.numpy(), pose=pose.numpy(),
+                        src=np.asarray(src, np.int64), dst=np.asarray(dst, np.int64),
+                        out_gcn1=outs[0].numpy(), out_gcn2=outs[1].numpy(),
+                        **{"gcn1." + k: v.numpy() for k, v in holder.gcn1.state_dict().items()})
+    print(f"ref_gcn_checkpoint: {os.path.getsize(path)} B")
+
+
 def main():
     models, utils = import_reference()
+    if "--checkpoint-only" in sys.argv:
+        make_checkpoint(models, utils)
+        return
     rng = np.random.RandomState(0)
 
     def frames(n, count, knn=None):
@@ -227,6 +275,7 @@ def main():
         quat=p1[:, 3:], so3=np.stack([utils.quat_to_so3(q) for q in p1[:, 3:]]),
     )
     print("relpose: selfcheck", utils.cal_relative_pose(a, b))
+    make_checkpoint(models, utils)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,129 @@
+"""Drop-in compatibility with the reference harness: a checkpoint pickled by the
+reference (``torch.save({'model': GCN ...})``, class path ``model.models.GCN``; the fixture
+``tests/golden/ref_gcn_checkpoint.pt`` was written by ``tests/golden/make_golden.py`` from the
+reference's own classes) unpickles into the MI355X classes through ``compat.reference_class_path``;
+``from dgl import batch`` / ``from model import models`` resolve; the reference's training-loop
+plumbing runs on the HIP path.  The fixture is our own file, so ``weights_only=False`` is allowed."""
+import os
+import subprocess
+import sys
+import types
+
+import numpy as np
+import pytest
+import torch
+
+import mrp_gnn_amd as m
+from conftest import GOLDEN_DIR, ROOT, load_golden, rel_err
+
+CKPT = os.path.join(GOLDEN_DIR, "ref_gcn_checkpoint.pt")
+
+
+def load_reference_checkpoint(**kw):
+    with m.compat.reference_class_path(**kw):
+        return torch.load(CKPT, weights_only=False)
+
+
+def test_reference_checkpoint_unpickles_into_native_classes():
+    saved = {k: sys.modules.get(k) for k in ("model", "model.models")}
+    ck = load_reference_checkpoint()
+    assert {k: sys.modules.get(k) for k in ("model", "model.models")} == saved  # aliases removed again
+    gcn = ck["model"]
+    assert type(gcn) is m.GCN and type(gcn.edge_encoder) is m.edge_encoder
+    assert ck["n_iter"] == 3
+    io = load_golden("ref_gcn_checkpoint_io")
+    sd = gcn.state_dict()
+    assert sorted(sd) == sorted(k[len("gcn1."):] for k in io if k.startswith("gcn1."))
+    for k, v in sd.items():
+        assert np.array_equal(v.numpy(), io["gcn1." + k])
+    stack = ck["stack"]
+    assert type(stack.gcn2) is m.GCN and stack.gcn1 is gcn
+    assert gcn.opt.feature_dim == 8 and gcn.opt.compress_gcn  # the reference's argparse opt travels along
+
+
+def test_models_alias_resolves_reference_only_names_through_fallback():
+    with m.compat.reference_class_path():
+        from model import models
+        assert models.GCN is m.GCN and models.multi_view_dgl_model is m.multi_view_dgl_model
+        with pytest.raises(AttributeError, match="fallback"):
+            models.decoder  # noqa: B018  (torchvision/dense-conv code, outside the hot path)
+    fb = types.SimpleNamespace(decoder="ref-decoder", GCN="not-used")
+    with m.compat.reference_class_path(fallback=fb):
+        from model import models
+        assert models.decoder == "ref-decoder" and models.GCN is m.GCN
+
+
+def test_dgl_alias_when_dgl_is_absent():
+    code = ("import sys; sys.path.insert(0, %r); import mrp_gnn_amd as m; m.compat.install();"
+            "from dgl import batch; import dgl;"
+            "g = batch([m.complete_graph(3), m.complete_graph(3)]);"
+            "assert batch is m.batch and dgl.DGLGraph is m.RobotGraph and g.num_nodes() == 6;"
+            "from model import models; assert models.GCN is m.GCN; print('ok')") % ROOT
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().endswith("ok")
+
+
+def test_collate_matches_dgl_batch_semantics():
+    rng = np.random.RandomState(0)
+    frames = []
+    for _ in range(3):
+        g = m.frame_graph(rng.rand(4, 7).astype(np.float32))
+        g.ndata["image"] = torch.randn(4, 2, 3, 3)
+        g.ndata["depth"] = torch.randn(4, 1, 8, 8)
+        frames.append(g)
+    b = m.compat.collate(frames)
+    assert b.batch_size == 3 and b.num_nodes() == 12 and b.num_edges() == 36
+    assert torch.equal(b.ndata["depth"][4:8], frames[1].ndata["depth"])
+    assert b.is_complete()
+
+
+@pytest.mark.gpu
+def test_reference_checkpoint_runs_on_the_hip_path(cuda_device):
+    ck = load_reference_checkpoint()
+    io = load_golden("ref_gcn_checkpoint_io")
+    g = m.RobotGraph(io["src"], io["dst"], num_nodes=io["x"].shape[0], batch_num_nodes=[4, 4],
+                     batch_num_edges=[12, 12])
+    g.ndata["image"] = torch.from_numpy(io["x"])
+    g.edata["pose"] = torch.from_numpy(io["pose"])
+    gd = g.to(cuda_device)
+    stack = ck["stack"].to(cuda_device)
+    with torch.no_grad():
+        assert rel_err(stack.gcn1(gd).cpu(), io["out_gcn1"]) <= 1e-5
+        assert rel_err(stack.gcn2(gd).cpu(), io["out_gcn2"]) <= 1e-5
+
+
+@pytest.mark.gpu
+def test_reference_training_loop_plumbing(cuda_device):
+    """``train_dgl`` (dgl/training.py:176-218) driven unchanged over the aliases: DataLoader with
+    the dgl.batch collate, ``data.to('cuda:0')``, ``model(data)``, backward, Adam step."""
+    opt = types.SimpleNamespace(feature_dim=16, compress_gcn=True, multi_gcn=True, camera_num=4, image_size=8,
+                                skip_level=False, task="depth")
+    with m.compat.reference_class_path():
+        from dgl import batch as dgl_batch  # noqa: F401  (what training.py imports, if DGL is absent)
+        from model import models
+        torch.manual_seed(0)
+        model = models.multi_view_dgl_model(opt).to(cuda_device)
+    rng = np.random.RandomState(1)
+    frames = []
+    for _ in range(6):
+        g = m.frame_graph(np.concatenate([rng.uniform(-5, 5, (4, 3)), rng.standard_normal((4, 4))], 1)
+                          .astype(np.float32))
+        g.ndata["image"] = torch.randn(4, 16, 8, 8)  # feature maps (the encoder is outside the hot path)
+        g.ndata["depth"] = torch.rand(4, 1, 8, 8)
+        frames.append(g)
+    loader = torch.utils.data.DataLoader(frames, batch_size=2, shuffle=False, collate_fn=m.compat.collate)
+    optimizer = torch.optim.Adam(model.parameters(), 0.005)
+    before = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    for data in loader:
+        optimizer.zero_grad()
+        data = data.to("cuda:0")
+        pred = model(data)
+        assert pred.shape == (8, 16, 8, 8)
+        loss = torch.nn.functional.smooth_l1_loss(pred[:, :1], data.ndata["depth"])
+        loss.backward()
+        optimizer.step()
+    after = model.state_dict()
+    for k in before:
+        assert torch.isfinite(after[k]).all()
+        assert not torch.equal(before[k], after[k]), f"{k} did not train"

@@ -255,6 +255,29 @@ int main(int argc, char** argv) {
   }
 
   if (N == 8 && !KNN) {
+    // occupancy sweep of the product forward: cap the workgroups per CU with padded LDS
+    const mrp_host::Geometry g = mrp_host::make_geometry(C, P, 4, 16, 64, mrp::kMaxChanPerBlock);
+    mrp::AggArgs a = args_for(g.lpc, g.cpb);
+    const int grid = B * a.ncb;
+    const size_t base = mrp_host::lds_fwd<8>(g.cpb);
+    for (int cap : {0, 2, 3, 4, 5, 6, 8}) {
+      const size_t lds = cap ? std::max(base, (size_t)(160 * 1024 / cap) - 256) : base;
+      char nm[64];
+      snprintf(nm, sizeof nm, "film_fwd occupancy cap=%d wg/cu lds=%zu", cap, lds);
+      float ms = time_ms([&] { hipLaunchKernelGGL((mrp::film_fwd<8, 4, true>), dim3(grid), dim3(g.threads), lds, 0, a); },
+                         iters);
+      report(nm, ms, alg);
+    }
+    for (int grid2 : {256, 512, 768}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "stream_copy f4 grid=%d", grid2);
+      float ms = time_ms([&] { hipLaunchKernelGGL(lab::stream_copy<mrp::f4>, dim3(grid2), dim3(256), 0, 0,
+                                                  (const mrp::f4*)x, (mrp::f4*)out, feat / 4); }, iters);
+      report(nm, ms, (double)feat * 8);
+    }
+  }
+
+  if (N == 8 && !KNN) {
     mrp::AggArgs a = args_for(64, 4);
     const int items = B * a.ncb;
     const size_t lds = (size_t)(2 * 4 * mrp::Tile<8>::SZ + 2 * mrp::Tile<8>::NTP) * 4;
