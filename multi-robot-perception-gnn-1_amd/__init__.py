@@ -12,7 +12,7 @@ from .aggregate import (FilmMeanFunction, film_mean, film_mean_cat, film_mean_ca
 from . import compat, compress, encoder  # noqa: F401
 from .device_graph import frame_batch  # noqa: F401
 from .graph import (GraphCSR, RobotGraph, batch, complete_edges, complete_graph, frame_graph,  # noqa: F401
-                    graph, knn_edges)
+                    graph, knn_edges, load_graphs, save_graphs, unbatch)
 from .models import GCN, GCNBlock, edge_encoder, multi_view_dgl_model  # noqa: F401
 from .pose import cal_relative_pose, quat_to_so3, relative_pose_batch  # noqa: F401
 

@@ -16,8 +16,11 @@ The reference harness touches this path through two imports and one file format:
   unpickles straight into them); every other name (the torchvision ``encoder``, ``decoder``,
   ``TransBlock``, the non-graph baselines — outside the hot path) is looked up in ``fallback``,
   the caller's own import of the reference ``models`` module, if one is given.
-* ``dgl`` (only when the real DGL is not importable) — ``batch``, ``graph`` and ``DGLGraph``
-  backed by :class:`~graph.RobotGraph`.
+* ``dgl`` (only when the real DGL is not importable) — ``batch``, ``unbatch``, ``graph`` and
+  ``DGLGraph`` backed by :class:`~graph.RobotGraph`; ``save_graphs``/``load_graphs`` for the dataset's
+  graph cache (``dgl/dataloader.py:165-175``; this package's own ``.npz``-based format — DGL's
+  binary format is not read, a DGL-written cache is rebuilt); ``dgl.data.DGLDataset``, the base
+  class of the reference's ``MultiViewDGLDataset``.
 
 With the aliases installed, the reference's own ``train_dgl``/``test_dgl`` loops run unchanged:
 the collate yields a :class:`~graph.RobotGraph`, ``.to('cuda:0')`` moves its features, and the
@@ -29,6 +32,7 @@ from __future__ import annotations
 
 import contextlib
 import importlib.util
+import os
 import sys
 import types
 from typing import Optional
@@ -63,13 +67,107 @@ def models_module(fallback: Optional[types.ModuleType] = None) -> types.ModuleTy
     return mod
 
 
+class DGLDataset:
+    """The ``dgl.data.DGLDataset`` lifecycle the reference dataset subclasses
+    (``dgl/dataloader.py:15-60,165-202``): the constructor records ``name``/``url``/``raw_dir``/
+    ``save_dir``/``force_reload``/``verbose`` and then loads — ``load()`` if ``has_cache()`` (and not
+    ``force_reload``), else ``download()``, ``process()``, ``save()``.  Restated from DGL's documented
+    behaviour (DGL itself is absent)."""
+
+    def __init__(self, name, url=None, raw_dir=None, save_dir=None, hash_key=(), force_reload=False,
+                 verbose=False):
+        self._name = name
+        self._url = url
+        self._raw_dir = raw_dir if raw_dir is not None else os.path.join(os.path.expanduser("~"), ".dgl")
+        self._save_dir = save_dir if save_dir is not None else self._raw_dir
+        self._hash_key = hash_key
+        self._force_reload = force_reload
+        self._verbose = verbose
+        self._load()
+
+    # the subclass API
+    def download(self):
+        pass
+
+    def process(self):
+        raise NotImplementedError
+
+    def save(self):
+        pass
+
+    def load(self):
+        pass
+
+    def has_cache(self):
+        return False
+
+    def __getitem__(self, idx):
+        raise NotImplementedError
+
+    def __len__(self):
+        raise NotImplementedError
+
+    # DGL's properties
+    @property
+    def name(self):
+        return self._name
+
+    @property
+    def url(self):
+        return self._url
+
+    @property
+    def raw_dir(self):
+        return self._raw_dir
+
+    @property
+    def save_dir(self):
+        return self._save_dir
+
+    @property
+    def raw_path(self):
+        return os.path.join(self._raw_dir, self._name)
+
+    @property
+    def save_path(self):
+        return os.path.join(self._save_dir, self._name)
+
+    @property
+    def verbose(self):
+        return self._verbose
+
+    def _load(self):
+        loaded = False
+        if not self._force_reload and self.has_cache():
+            try:
+                self.load()
+                loaded = True
+            except (OSError, ValueError, KeyError) as e:  # stale / foreign cache: rebuild it
+                if self._verbose:
+                    print(f"[{self._name}] cache not loadable ({e}); processing again")
+        if not loaded:
+            os.makedirs(self._raw_dir, exist_ok=True)
+            self.download()
+            self.process()
+            os.makedirs(self._save_dir, exist_ok=True)
+            self.save()
+
+
 def dgl_module() -> types.ModuleType:
-    """The slice of the ``dgl`` namespace the harness imports on this path."""
+    """The slice of the ``dgl`` namespace the reference touches on this path: ``batch`` (collate),
+    ``graph``, ``save_graphs``/``load_graphs`` (dataset cache, this package's own format),
+    ``unbatch``, ``DGLGraph`` and ``dgl.data.DGLDataset``."""
     mod = types.ModuleType("dgl")
     mod.__doc__ = "mrp_gnn_amd stand-in for dgl (batch / graph / DGLGraph on RobotGraph)"
+    mod.__path__ = []
     mod.batch = _graph.batch
+    mod.unbatch = _graph.unbatch
     mod.graph = _graph.graph
+    mod.save_graphs = _graph.save_graphs
+    mod.load_graphs = _graph.load_graphs
     mod.DGLGraph = _graph.RobotGraph
+    mod.data = types.ModuleType("dgl.data")
+    mod.data.DGLDataset = DGLDataset
     return mod
 
 
@@ -83,7 +181,7 @@ def _dgl_importable() -> bool:
 def install(fallback: Optional[types.ModuleType] = None, dgl: bool = True) -> dict:
     """Register the ``model.models`` (and, if DGL is absent, ``dgl``) aliases in ``sys.modules``.
     Returns the previous entries, for :func:`uninstall`."""
-    saved = {k: sys.modules.get(k) for k in ("model", "model.models", "dgl")}
+    saved = {k: sys.modules.get(k) for k in ("model", "model.models", "dgl", "dgl.data")}
     pkg = types.ModuleType("model")
     pkg.__path__ = []  # a package, so ``from model import models`` and pickle's import both work
     pkg.models = models_module(fallback)
@@ -91,6 +189,7 @@ def install(fallback: Optional[types.ModuleType] = None, dgl: bool = True) -> di
     sys.modules["model.models"] = pkg.models
     if dgl and not _dgl_importable():
         sys.modules["dgl"] = dgl_module()
+        sys.modules["dgl.data"] = sys.modules["dgl"].data
     return saved
 
 

@@ -375,3 +375,79 @@ def batch(graphs: Iterable[RobotGraph]) -> RobotGraph:
 def unbatch_offsets(g: RobotGraph):
     """Node offsets of the graphs in a batch (int64 numpy, length batch_size + 1)."""
     return np.concatenate([[0], np.cumsum(g._bnn)]).astype(np.int64)
+
+
+def unbatch(g: RobotGraph) -> List[RobotGraph]:
+    """``dgl.unbatch`` equivalent: split a batched graph into its per-frame graphs (node and edge
+    ids renumbered from 0 per graph, features sliced)."""
+    src, dst = (t.numpy() for t in g.edges())
+    noff = np.concatenate([[0], np.cumsum(g._bnn)]).astype(np.int64)
+    eoff = np.concatenate([[0], np.cumsum(g._bne)]).astype(np.int64)
+    out = []
+    for i in range(len(g._bnn)):
+        e0, e1, n0, n1 = eoff[i], eoff[i + 1], noff[i], noff[i + 1]
+        s, d = src[e0:e1] - n0, dst[e0:e1] - n0
+        if s.size and (s.min() < 0 or d.min() < 0 or s.max() >= n1 - n0 or d.max() >= n1 - n0):
+            raise ValueError(f"graph {i}: its edges leave its node range (not a dgl.batch result)")
+        gi = RobotGraph(s, d, num_nodes=int(n1 - n0))
+        for k, v in g.ndata.items():
+            gi.ndata[k] = v[n0:n1]
+        for k, v in g.edata.items():
+            gi.edata[k] = v[e0:e1]
+        out.append(gi)
+    return out
+
+
+# ------------------------------------------------------------------ graph cache on disk
+_CACHE_MAGIC = "mrp_gnn_graph_cache_v1"
+
+
+def save_graphs(filename: str, g_list, labels: Optional[Dict[str, torch.Tensor]] = None) -> None:
+    """``dgl.save_graphs`` equivalent for the dataset cache (``dgl/dataloader.py:165-169``).
+
+    Format: a NumPy ``.npz`` archive (no pickles) written to ``filename`` as given — the batched
+    structure (src, dst, per-graph node/edge counts) plus every node/edge feature and label.  This is
+    this package's own cache format; DGL's binary ``save_graphs`` format is not read (DGL is not
+    available here and the reference ships no cache file to pin it against), so a cache written by
+    DGL must be rebuilt — the reference dataset does that when ``has_cache()`` is False."""
+    g_list = [g_list] if isinstance(g_list, RobotGraph) else list(g_list)
+    arrays = {"magic": np.array(_CACHE_MAGIC), "num_graphs": np.array(len(g_list), np.int64)}
+    if g_list:
+        b = batch(g_list)
+        src, dst = (t.numpy() for t in b.edges())
+        arrays.update(src=src, dst=dst, bnn=np.asarray(b._bnn, np.int64), bne=np.asarray(b._bne, np.int64))
+        for k, v in b.ndata.items():
+            arrays["ndata/" + k] = v.detach().cpu().numpy()
+        for k, v in b.edata.items():
+            arrays["edata/" + k] = v.detach().cpu().numpy()
+    for k, v in (labels or {}).items():
+        arrays["label/" + k] = torch.as_tensor(v).detach().cpu().numpy()
+    with open(filename, "wb") as f:
+        np.savez(f, **arrays)
+
+
+def load_graphs(filename: str, idx_list: Optional[Sequence[int]] = None):
+    """``dgl.load_graphs`` equivalent: ``(list of graphs, labels dict)`` from :func:`save_graphs`'s
+    format (``dgl/dataloader.py:172-175``); ``idx_list`` selects graphs by index."""
+    try:
+        z = np.load(filename, allow_pickle=False)
+    except ValueError as e:
+        raise ValueError(f"{filename}: not an mrp_gnn graph cache (DGL's binary format is not read; "
+                         "delete the file so the dataset rebuilds it)") from e
+    with z:
+        if "magic" not in z.files or str(z["magic"]) != _CACHE_MAGIC:
+            raise ValueError(f"{filename}: not an mrp_gnn graph cache")
+        labels = {k[len("label/"):]: torch.from_numpy(z[k]) for k in z.files if k.startswith("label/")}
+        if int(z["num_graphs"]) == 0:
+            return [], labels
+        bnn, bne = z["bnn"].tolist(), z["bne"].tolist()
+        b = RobotGraph(z["src"], z["dst"], num_nodes=int(sum(bnn)), batch_num_nodes=bnn, batch_num_edges=bne)
+        for k in z.files:
+            if k.startswith("ndata/"):
+                b.ndata[k[len("ndata/"):]] = torch.from_numpy(z[k])
+            elif k.startswith("edata/"):
+                b.edata[k[len("edata/"):]] = torch.from_numpy(z[k])
+    graphs = unbatch(b)
+    if idx_list is not None:
+        graphs = [graphs[i] for i in idx_list]
+    return graphs, labels

@@ -127,3 +127,81 @@ def test_reference_training_loop_plumbing(cuda_device):
     for k in before:
         assert torch.isfinite(after[k]).all()
         assert not torch.equal(before[k], after[k]), f"{k} did not train"
+
+
+def test_graph_cache_round_trip(tmp_path):
+    rng = np.random.RandomState(2)
+    graphs = []
+    for n in (3, 5, 4):
+        g = m.frame_graph(rng.rand(n, 7).astype(np.float32), knn=2 if n == 5 else None)
+        g.ndata["image"] = torch.randn(n, 3, 4, 4)
+        g.ndata["seg"] = torch.randint(0, 7, (n, 1, 4, 4))
+        graphs.append(g)
+    path = str(tmp_path / "dgl_graph_5.bin")  # the reference's file name (dataloader.py:168)
+    m.save_graphs(path, graphs, {"glabel": torch.arange(3)})
+    back, labels = m.load_graphs(path)
+    assert torch.equal(labels["glabel"], torch.arange(3))
+    assert len(back) == 3
+    for a, b in zip(graphs, back):
+        assert a.num_nodes() == b.num_nodes() and a.num_edges() == b.num_edges()
+        for t, u in zip(a.edges(), b.edges()):
+            assert torch.equal(t, u)
+        for k in a.ndata:
+            assert torch.equal(a.ndata[k], b.ndata[k]) and a.ndata[k].dtype == b.ndata[k].dtype
+        assert torch.equal(a.edata["pose"], b.edata["pose"])
+    sel, _ = m.load_graphs(path, [2, 0])
+    assert [g.num_nodes() for g in sel] == [4, 3]
+    assert m.unbatch(m.batch(back))[1].num_edges() == graphs[1].num_edges()
+    foreign = tmp_path / "dgl_written.bin"
+    foreign.write_bytes(b"\x3f\xa1\xb4\x46\xf0\x4f\x2e\xdd" + bytes(64))
+    with pytest.raises(ValueError, match="not an mrp_gnn graph cache"):
+        m.load_graphs(str(foreign))
+
+
+def test_dataset_lifecycle_like_the_reference(tmp_path):
+    """A subclass shaped like MultiViewDGLDataset (dgl/dataloader.py:15-202): processes and saves on
+    the first construction, loads the cache on the second; a foreign cache is rebuilt."""
+    with m.compat.reference_class_path():
+        from dgl import load_graphs, save_graphs
+        from dgl.data import DGLDataset
+    calls = []
+
+    class Frames(DGLDataset):
+        def __init__(self, save_dir):
+            super().__init__(name="FlightmareDGL", raw_dir=str(tmp_path / "raw"), save_dir=save_dir)
+
+        def process(self):
+            calls.append("process")
+            self.graphs = [m.complete_graph(4) for _ in range(3)]
+            for g in self.graphs:
+                g.ndata["image"] = torch.ones(4, 2)
+
+        def path(self):
+            return os.path.join(self.save_dir, "dgl_graph_4.bin")
+
+        def save(self):
+            calls.append("save")
+            save_graphs(self.path(), self.graphs)
+
+        def load(self):
+            calls.append("load")
+            self.graphs, _ = load_graphs(self.path())
+
+        def has_cache(self):
+            return os.path.exists(self.path())
+
+        def __getitem__(self, i):
+            return self.graphs[i]
+
+        def __len__(self):
+            return len(self.graphs)
+
+    d1 = Frames(str(tmp_path / "proc"))
+    d2 = Frames(str(tmp_path / "proc"))
+    assert calls == ["process", "save", "load"]
+    assert len(d2) == 3 and d2[1].num_edges() == 12 and torch.equal(d2[2].ndata["image"], torch.ones(4, 2))
+    assert d1.save_dir == str(tmp_path / "proc") and d1.name == "FlightmareDGL"
+    (tmp_path / "proc" / "dgl_graph_4.bin").write_bytes(b"not ours")
+    calls.clear()
+    Frames(str(tmp_path / "proc"))
+    assert calls == ["load", "process", "save"]
