@@ -107,6 +107,35 @@ def cpu_baseline(N, C, H, W, seconds, sample_graphs):
                       f"torch CPU fp32, {threads} threads"}
 
 
+def graph_build_time(B, N, device, reps=20):
+    """Per-batch graph construction: the device builder (``frame_batch``: one kernel for edge list,
+    relative poses and CSR) against the host path the reference's dataset runs (per-frame
+    ``cal_relative_pose`` + ``dgl.batch``, restated by ``frame_graph`` + ``batch``)."""
+    rng = np.random.RandomState(7)
+    t = rng.uniform(-10, 10, size=(B, N, 3))
+    q = rng.standard_normal((B, N, 4))
+    q /= np.linalg.norm(q, axis=-1, keepdims=True)
+    poses = np.concatenate([t, q], -1).astype(np.float32)
+    pd = torch.from_numpy(poses).to(device)
+    for _ in range(3):
+        mrp.frame_batch(pd)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g = mrp.frame_batch(pd)
+    torch.cuda.synchronize(device)
+    dev_s = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(3):
+        gh = mrp.batch([mrp.frame_graph(p) for p in poses]).to(device)
+        gh.csr(device)
+    torch.cuda.synchronize(device)
+    host_s = (time.perf_counter() - t0) / 3
+    assert torch.equal(g.edata["pose"].cpu(), gh.edata["pose"].cpu())
+    return {"what": f"build B={B} complete {N}-robot frame graphs (edge poses + CSR), ready on the device",
+            "device_us": dev_s * 1e6, "host_us": host_s * 1e6}
+
+
 def pmc_traffic(workload):
     """Per-launch HBM bytes from a committed rocprofv3 PMC summary for this workload, if any."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")))
@@ -259,6 +288,7 @@ def main():
     if not args.no_train:
         train = train_step_time(gcn, g, x, world, device, args)
     block = None if args.no_block else block_step_time(world, device, args, rank)
+    gbuild = graph_build_time(B, N, device)
 
     elems_per_step = Nt * C * P
     value = world * elems_per_step * args.steps / elapsed
@@ -297,6 +327,7 @@ def main():
         }
     if block is not None:
         result["block_step"] = block
+    result["graph_build"] = gbuild
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(N, C, H, W, args.cpu_seconds, args.cpu_sample_graphs)
     if rank == 0:

@@ -9,11 +9,11 @@ cd /tmp && export TMPDIR=/tmp
 cd "$ROOT"
 OUT=gpurun_out/prof_$R
 mkdir -p "$OUT"
-BENCH_ARGS="--steps 20 --warmup 5 --kernel-iters 20 --no-cpu-baseline"
+BENCH_ARGS="--steps 20 --warmup 5 --kernel-iters 20 --no-cpu-baseline --no-block"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
   -- python3 bench.py $BENCH_ARGS > "$OUT/bench_trace.log" 2>&1
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "film_" -d "$OUT/pmc_$C" -o run --output-format csv \
-    -- python3 bench.py --steps 3 --warmup 1 --kernel-iters 3 --no-cpu-baseline > "$OUT/pmc_$C.log" 2>&1
+    -- python3 bench.py --steps 3 --warmup 1 --kernel-iters 3 --no-cpu-baseline --no-block > "$OUT/pmc_$C.log" 2>&1
 done
 echo "profile $R done"
