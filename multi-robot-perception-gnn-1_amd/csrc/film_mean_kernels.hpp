@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
+#include <type_traits>
 
 #include "mrp_gnn.h"
 
@@ -145,6 +146,18 @@ __device__ __forceinline__ int64_t complete_eid(int64_t ebase, int n, int u, int
   return ebase + (int64_t)u * (n - 1) + (v < u ? v : v - 1);
 }
 
+// t -> (channel within the block, rest) with channel fastest.  cpb is wave-uniform and almost always
+// a power of two: then a mask and a shift instead of an integer division.
+__device__ __forceinline__ void split_channel(const AggArgs& a, int t, int& cl, int& rest) {
+  if ((a.cpb & (a.cpb - 1)) == 0) {
+    cl = t & (a.cpb - 1);
+    rest = t >> __builtin_ctz((unsigned)a.cpb);
+  } else {
+    cl = t % a.cpb;
+    rest = t / a.cpb;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Prologue, CSR graphs: dense per-channel weight tiles from the CSR-by-destination graph.
 //
@@ -170,8 +183,8 @@ __device__ __forceinline__ void build_tiles_csr(const AggArgs& a, int node0, int
   }
   __syncthreads();
   for (int t = tid; t < a.cpb * NT; t += nth) {
-    const int cl = t % a.cpb;  // channel fastest: neighbouring lanes read neighbouring gb pairs
-    const int v = t / a.cpb;
+    int cl, v;  // channel fastest: neighbouring lanes read neighbouring gb pairs
+    split_channel(a, t, cl, v);
     const int c = c0 + cl;
     if (v < n && c < a.C) {
       const int beg = a.indptr[node0 + v];
@@ -246,8 +259,8 @@ __device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, 
     const int t = base + threadIdx.x + r * blockDim.x;
     float2 val = make_float2(0.f, 0.f);
     if (t < tot) {
-      const int cl = t % a.cpb;  // channel fastest -> neighbouring lanes read neighbouring pairs
-      const int slot = t / a.cpb;
+      int cl, slot;  // channel fastest -> neighbouring lanes read neighbouring pairs
+      split_channel(a, t, cl, slot);
       const int v = slot / NT, u = slot - v * NT;
       const int c = c0 + cl;
       if (u != v && c < a.C) {
@@ -275,8 +288,8 @@ __device__ __forceinline__ void complete_store(const AggArgs& a, int base, const
   for (int r = 0; r < CompleteSlots<NT>::kPer; ++r) {
     const int t = base + threadIdx.x + r * blockDim.x;
     if (t < tot) {
-      const int cl = t % a.cpb;
-      const int slot = t / a.cpb;
+      int cl, slot;
+      split_channel(a, t, cl, slot);
       const int v = slot / NT, u = slot - v * NT;
       if (BWD) {
         Ga[cl * SZ + u * NTP + v] = s * reg[r].x;
@@ -504,14 +517,31 @@ __device__ __forceinline__ float dpp_mov(float x) {
 // of the group ends with the sum.  Butterfly: xor 1 and xor 2 by quad_perm, 4 <-> 4 by
 // row_half_mirror, 8 <-> 8 by row_mirror (all DPP modifiers on the add), then xor 16 / xor 32 by
 // ds_bpermute.  Steps wider than the group are skipped by a uniform branch.
-__device__ __forceinline__ float group_sum(float x, int lpc) {
-  if (lpc >= 2) x += dpp_mov<0xB1>(x);   // quad_perm [1,0,3,2]
-  if (lpc >= 4) x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]
-  if (lpc >= 8) x += dpp_mov<0x141>(x);  // row_half_mirror
-  if (lpc >= 16) x += dpp_mov<0x140>(x);  // row_mirror
-  if (lpc >= 32) x += __shfl_xor(x, 16, 64);
-  if (lpc >= 64) x += __shfl_xor(x, 32, 64);
+template <int L>
+__device__ __forceinline__ float group_sum(float x) {
+  if constexpr (L >= 2) x += dpp_mov<0xB1>(x);   // quad_perm [1,0,3,2]
+  if constexpr (L >= 4) x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]
+  if constexpr (L >= 8) x += dpp_mov<0x141>(x);  // row_half_mirror
+  if constexpr (L >= 16) x += dpp_mov<0x140>(x);  // row_mirror
+  if constexpr (L >= 32) x += __shfl_xor(x, 16, 64);
+  if constexpr (L >= 64) x += __shfl_xor(x, 32, 64);
   return x;
+}
+
+// Call f(std::integral_constant<int, L>) with L = lpc: the lane count is wave-uniform but only
+// known at run time, so branch once here rather than once per reduced value (a runtime-width
+// butterfly costs a scalar compare and branch per step per value).
+template <class F>
+__device__ __forceinline__ void with_lanes(int lpc, F&& f) {
+  switch (lpc) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 16: f(std::integral_constant<int, 16>{}); break;
+    case 32: f(std::integral_constant<int, 32>{}); break;
+    default: f(std::integral_constant<int, 64>{}); break;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -649,15 +679,18 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
     if (a.want_dgb) {
       // Reduce across the lanes of each channel group (all lanes of the wave take part in the
       // shuffles; inactive groups contribute zeros to their own group).
+      with_lanes(a.lpc, [&](auto lanes) {
+        constexpr int L = decltype(lanes)::value;
 #pragma unroll
-      for (int i = 0; i < VB; ++i) {
-        S[i] = group_sum(S[i], a.lpc);
+        for (int i = 0; i < VB; ++i) {
+          S[i] = group_sum<L>(S[i]);
 #pragma unroll
-        for (int u = 0; u < NT; ++u) {
-          if (COMPLETE && kOnePass && u == i) continue;
-          D[i][u] = group_sum(D[i][u], a.lpc);
+          for (int u = 0; u < NT; ++u) {
+            if (COMPLETE && kOnePass && u == i) continue;
+            D[i][u] = group_sum<L>(D[i][u]);
+          }
         }
-      }
+      });
       if (active && li == 0) {
 #pragma unroll
         for (int i = 0; i < VB; ++i) {
@@ -678,8 +711,8 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
     const float s = (a.mode != MRP_AGG_FILM_SUM && NT > 1) ? 1.f / (float)(NT - 1) : 1.f;
     const int64_t ebase = (int64_t)b * NT * (NT - 1);
     for (int t = threadIdx.x; t < a.cpb * NT * NT; t += blockDim.x) {
-      const int cl = t % a.cpb;
-      const int slot = t / a.cpb;
+      int cl, slot;
+      split_channel(a, t, cl, slot);
       const int v = slot / NT, u = slot - v * NT;
       const int cc = c0 + cl;
       if (u == v || cc >= a.C) continue;
@@ -698,8 +731,8 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   // Every edge of the graph has exactly one destination here, so each grad_gb element is
   // written once.
   for (int t = threadIdx.x; t < a.cpb * NT; t += blockDim.x) {
-    const int cl = t % a.cpb;
-    const int v = t / a.cpb;
+    int cl, v;
+    split_channel(a, t, cl, v);
     const int cc = c0 + cl;
     if (v >= n || cc >= a.C) continue;
     const int beg = a.indptr[node0 + v];
@@ -847,12 +880,15 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
     }
   }
   if (!a.want_dgb) return;
+  with_lanes(a.lpc, [&](auto lanes) {
+    constexpr int L = decltype(lanes)::value;
 #pragma unroll
-  for (int v = 0; v < NT; ++v) {
-    S[v] = group_sum(S[v], a.lpc);
+    for (int v = 0; v < NT; ++v) {
+      S[v] = group_sum<L>(S[v]);
 #pragma unroll
-    for (int jj = 0; jj < KMAX; ++jj) D[v * KMAX + jj] = group_sum(D[v * KMAX + jj], a.lpc);
-  }
+      for (int jj = 0; jj < KMAX; ++jj) D[v * KMAX + jj] = group_sum<L>(D[v * KMAX + jj]);
+    }
+  });
   if (active && li == 0) {
 #pragma unroll
     for (int v = 0; v < NT; ++v) {
@@ -864,8 +900,8 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
   __syncthreads();
   // per-edge outputs: thread -> (channel fastest, slot)
   for (int t = threadIdx.x; t < a.cpb * NS; t += blockDim.x) {
-    const int cl = t % a.cpb;
-    const int slot = t / a.cpb;
+    int cl, slot;
+    split_channel(a, t, cl, slot);
     const int v = slot / KMAX;
     const int cc = c0 + cl;
     const int e = slot_e[slot];

@@ -407,6 +407,35 @@ int main(int argc, char** argv) {
     }
     CK(hipFree(dgb));
   }
+  if (N == 8 && !KNN) {
+    // fused backward: slice width x occupancy floor (MINW = waves per SIMD the compiler must fit)
+    float* dgb2;
+    CK(hipMalloc(&dgb2, (size_t)E * C * 2 * 4));
+    const double bwd_bytes = (double)feat * 12 + (double)E * C * 2 * 8;
+    auto run = [&](auto kern, int vec, int lpc, int minw) {
+      if (lpc > P / vec) return;
+      const int cpb = std::min(C, std::min(256 / lpc, 32));
+      mrp::AggArgs a = {};
+      a.x = x; a.xs = (int64_t)C * P; a.gb = gb; a.goff = d_goff; a.out = out; a.os = (int64_t)C * P;
+      a.C = C; a.P = P; a.PV = P / vec; a.mode = 0; a.lpc = lpc; a.cpb = cpb; a.ncb = (C + cpb - 1) / cpb;
+      a.logits = 1; a.g = gout; a.gs = (int64_t)C * P; a.dgb = dgb2; a.want_dx = 1; a.want_dgb = 1;
+      const int grid = B * a.ncb;
+      const size_t lds = mrp_host::lds_bwd<8>(cpb, true);
+      float ms = time_ms([&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(cpb * lpc), lds, 0, a); }, iters);
+      char nm[96];
+      snprintf(nm, sizeof nm, "bwd_fused vec=%d minw=%d lpc=%d cpb=%d", vec, minw, lpc, cpb);
+      report(nm, ms, bwd_bytes);
+    };
+    for (int lpc : {4, 8, 16, 32}) {
+      run(mrp::film_bwd_fused<8, 8, 4, true, false, 1>, 4, lpc, 1);
+      run(mrp::film_bwd_fused<8, 8, 4, true, false, 2>, 4, lpc, 2);
+      run(mrp::film_bwd_fused<8, 8, 4, true, false, 3>, 4, lpc, 3);
+      run(mrp::film_bwd_fused<8, 8, 2, true, false, 1>, 2, lpc, 1);
+      run(mrp::film_bwd_fused<8, 8, 2, true, false, 3>, 2, lpc, 3);
+      run(mrp::film_bwd_fused<8, 8, 2, true, false, 4>, 2, lpc, 4);
+    }
+    CK(hipFree(dgb2));
+  }
   // product entry points (default geometry), both graph kinds
   float* dgb_prod;
   CK(hipMalloc(&dgb_prod, (size_t)E * C * 2 * 4));
