@@ -57,7 +57,9 @@ enum mrp_graph_kind {
 };
 /* MRP_GRAPH_REGULAR(k): a CSR graph in which every node has exactly k in-edges (k-NN graphs).  The
  * CSR arrays are read as for MRP_GRAPH_CSR; the backward for graphs of more than 8 nodes then keeps
- * one Gram accumulator per edge instead of per node pair (k <= 8).  num_edges must be k*num_nodes. */
+ * one Gram accumulator per edge instead of per node pair (k <= 8).  num_edges must be k*num_nodes.
+ * Node v's CSR row is then [k*v, k*(v+1)) by construction (CSR by destination, uniform degree), so
+ * the forward does not read indptr. */
 #define MRP_GRAPH_REGULAR(k) (((k) << 8) | 2)
 #define MRP_GRAPH_IS_REGULAR(kind) (((kind) & 0xff) == 2)
 #define MRP_GRAPH_REGULAR_K(kind) ((kind) >> 8)
@@ -150,6 +152,21 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride,
  */
 int mrp_edge_hidden_fwd(const float* pose, const float* w1, const float* b1,
                         int32_t num_edges, int32_t C, float* h, void* stream);
+
+/*
+ * Backward of the edge encoder's reductions (dgl/model/models.py:147-149), run after the two
+ * library GEMMs of its backward (dh = dz W2, dW2 = dz^T h):
+ *   db2[j]    = sum_e dz[e, j]                              (dz: (E, 2C), the logits' gradient that
+ *                                                            mrp_film_mean_bwd writes with MRP_AGG_GB_LOGITS)
+ *   dw1[k, i] = sum_e dh[e, k] * [h[e, k] > 0] * pose[e, i] (dh, h: (E, C); pose (E, 9); dw1 (C, 9))
+ *   db1[k]    = sum_e dh[e, k] * [h[e, k] > 0]
+ * workspace: device buffer of mrp_edge_encoder_bwd_workspace(E, C) bytes.  Outputs may be NULL.
+ * Deterministic (fixed summation order, no atomics).
+ */
+int64_t mrp_edge_encoder_bwd_workspace(int32_t num_edges, int32_t C);
+int mrp_edge_encoder_bwd(const float* dz, const float* dh, const float* h, const float* pose,
+                         int32_t num_edges, int32_t C, float* db2, float* dw1, float* db1,
+                         float* workspace, void* stream);
 
 /*
  * Per-frame robot graphs built on the device (dgl/dataloader.py:88-122 with the relative pose of

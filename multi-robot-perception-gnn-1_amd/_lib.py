@@ -23,11 +23,13 @@ EXPORTED_SYMBOLS = (
     "mrp_film_mean_cat_fwd",
     "mrp_film_mean_bwd",
     "mrp_edge_hidden_fwd",
+    "mrp_edge_encoder_bwd_workspace",
+    "mrp_edge_encoder_bwd",
     "mrp_frame_graph_build",
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_NODES = 16
 
 MODE_FILM_MEAN = 0
@@ -64,6 +66,10 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_film_mean_bwd.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
+    lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]
+    lib.mrp_edge_encoder_bwd_workspace.restype = ctypes.c_int64
+    lib.mrp_edge_encoder_bwd.argtypes = [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P]
+    lib.mrp_edge_encoder_bwd.restype = ctypes.c_int
     lib.mrp_frame_graph_build.argtypes = [_P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]
     lib.mrp_frame_graph_build.restype = ctypes.c_int
     lib.mrp_abi_version.argtypes = []

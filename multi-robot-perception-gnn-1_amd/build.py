@@ -26,21 +26,30 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build the HIP library)")
 
 
+def _obj(src: str) -> str:
+    return os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+
+
+def _stale(src: str) -> bool:
+    obj = _obj(src)
+    return not os.path.exists(obj) or os.path.getmtime(obj) <= max(os.path.getmtime(d) for d in [src] + HEADERS)
+
+
 def needs_build(out: str = OUT) -> bool:
-    if not os.path.exists(out):
+    """The library is missing, an object is older than its source or a header, or the library is
+    older than an object (freshness is judged per object, not against the library)."""
+    if not os.path.exists(out) or any(_stale(s) for s in SOURCES):
         return True
     t = os.path.getmtime(out)
-    deps = SOURCES + HEADERS
-    return any(os.path.getmtime(s) > t for s in deps)
+    return any(os.path.getmtime(_obj(s)) > t for s in SOURCES)
 
 
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mcode-object-version=5", "-ffp-contract=off", "-Wno-pass-failed"]
 
 
 def _compile(src: str, verbose: bool) -> str:
-    obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
-    deps = [src] + HEADERS
-    if os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(d) for d in deps):
+    obj = _obj(src)
+    if not _stale(src):
         return obj
     cmd = [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + ["-I", os.path.join(REPO, "include"), "-c", src,
                                                       "-o", obj + ".tmp"]

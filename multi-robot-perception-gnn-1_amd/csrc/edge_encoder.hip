@@ -78,3 +78,101 @@ extern "C" int mrp_edge_hidden_fwd(const float* pose, const float* w1, const flo
 #undef MRP_HIDDEN
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Backward of the encoder's small reductions (dgl/model/models.py:147-149), after the two library
+// GEMMs dh = dz W2 and dW2 = dz^T h:
+//   db2[j]    = sum_e dz[e, j]                         (2C columns)
+//   dw1[k, i] = sum_e dh[e, k] [h[e, k] > 0] pose[e, i] (ReLU backward folded in)
+//   db1[k]    = sum_e dh[e, k] [h[e, k] > 0]
+// Torch runs these as compare + mul + a K = E GEMM + two column reductions (five launches).  Here:
+// pass 1 = one thread per output column per chunk of kRows edges (coalesced row reads, the 9 pose
+// values wave-uniform), partial sums to a workspace; pass 2 = the sum over chunks in chunk order.
+// Deterministic: no atomics, a fixed summation order.
+// ---------------------------------------------------------------------------------------------
+namespace mrp_enc {
+
+constexpr int kRows = 64;  // edges per chunk
+
+// workspace row per chunk: [0, 2C) db2 partials, then per hidden unit k: 9 dw1 + 1 db1 partials
+__global__ void __launch_bounds__(256) encoder_bwd_partial(const float* __restrict__ dz, const float* __restrict__ dh,
+                                                           const float* __restrict__ h, const float* __restrict__ pose,
+                                                           int E, int C, float* __restrict__ ws) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;  // [0, 2C): dz column, [2C, 3C): hidden unit
+  const int chunk = blockIdx.y;
+  const int e0 = chunk * kRows;
+  const int e1 = min(E, e0 + kRows);
+  float* out = ws + (int64_t)chunk * 12 * C;
+  if (col < 2 * C) {
+    float acc = 0.f;
+    for (int e = e0; e < e1; ++e) acc += dz[(int64_t)e * 2 * C + col];
+    out[col] = acc;
+  } else if (col < 3 * C) {
+    const int k = col - 2 * C;
+    float acc[NIN + 1];
+#pragma unroll
+    for (int i = 0; i <= NIN; ++i) acc[i] = 0.f;
+    for (int e = e0; e < e1; ++e) {
+      const float g = dh[(int64_t)e * C + k];
+      const float d = h[(int64_t)e * C + k] > 0.f ? g : 0.f;
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) acc[i] = fmaf(d, pose[(int64_t)e * NIN + i], acc[i]);
+      acc[NIN] += d;
+    }
+#pragma unroll
+    for (int i = 0; i <= NIN; ++i) out[2 * C + k * (NIN + 1) + i] = acc[i];
+  }
+}
+
+__global__ void __launch_bounds__(256) encoder_bwd_final(const float* __restrict__ ws, int nchunks, int C,
+                                                         float* __restrict__ db2, float* __restrict__ dw1,
+                                                         float* __restrict__ db1) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 12 * C) return;
+  float acc = 0.f;
+  for (int c = 0; c < nchunks; ++c) acc += ws[(int64_t)c * 12 * C + t];
+  if (t < 2 * C) {
+    if (db2) db2[t] = acc;
+  } else {
+    const int k = (t - 2 * C) / (NIN + 1), i = (t - 2 * C) - k * (NIN + 1);
+    if (i < NIN) {
+      if (dw1) dw1[(int64_t)k * NIN + i] = acc;
+    } else if (db1) {
+      db1[k] = acc;
+    }
+  }
+}
+
+}  // namespace mrp_enc
+
+extern "C" int64_t mrp_edge_encoder_bwd_workspace(int32_t num_edges, int32_t C) {
+  if (num_edges <= 0 || C <= 0) return 0;
+  const int64_t nchunks = ((int64_t)num_edges + mrp_enc::kRows - 1) / mrp_enc::kRows;
+  return nchunks * 12 * (int64_t)C * (int64_t)sizeof(float);
+}
+
+extern "C" int mrp_edge_encoder_bwd(const float* dz, const float* dh, const float* h, const float* pose,
+                                    int32_t num_edges, int32_t C, float* db2, float* dw1, float* db1,
+                                    float* workspace, void* stream) {
+  if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (C == 0) return hipSuccess;
+  if (num_edges == 0) {  // empty sums
+    hipError_t e = hipSuccess;
+    if (db2) e = hipMemsetAsync(db2, 0, sizeof(float) * 2 * (size_t)C, st);
+    if (e == hipSuccess && dw1) e = hipMemsetAsync(dw1, 0, sizeof(float) * mrp_enc::NIN * (size_t)C, st);
+    if (e == hipSuccess && db1) e = hipMemsetAsync(db1, 0, sizeof(float) * (size_t)C, st);
+    return e;
+  }
+  if (!dz || !dh || !h || !pose || !workspace) return hipErrorInvalidValue;
+  if ((int64_t)C * 12 > 0x7fffffff / 2) return hipErrorInvalidValue;
+  const int nchunks = (num_edges + mrp_enc::kRows - 1) / mrp_enc::kRows;
+  if (nchunks > 65535) return hipErrorInvalidValue;  // grid.y limit: E up to ~4.2M edges
+  hipLaunchKernelGGL(mrp_enc::encoder_bwd_partial, dim3((3 * C + 255) / 256, nchunks), dim3(256), 0, st, dz, dh, h,
+                     pose, num_edges, C, workspace);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(mrp_enc::encoder_bwd_final, dim3((12 * C + 255) / 256), dim3(256), 0, st, workspace, nchunks, C,
+                     db2, dw1, db1);
+  return hipGetLastError();
+}

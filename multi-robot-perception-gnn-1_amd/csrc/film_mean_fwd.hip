@@ -27,7 +27,7 @@ hipError_t dispatch_fwd(int nt, bool complete, const AggArgs& a, const Geometry&
 
 extern "C" {
 
-int mrp_abi_version(void) { return 8; }
+int mrp_abi_version(void) { return 9; }
 
 const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
 
@@ -77,6 +77,7 @@ int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const 
   a.logits = logits;
   a.xc = xcopy;
   a.xcs = xcopy_node_stride;
+  a.kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
   return dispatch_fwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, static_cast<hipStream_t>(stream));
 }
 

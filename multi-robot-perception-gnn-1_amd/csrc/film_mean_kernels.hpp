@@ -187,8 +187,10 @@ __device__ __forceinline__ void build_tiles_csr(const AggArgs& a, int node0, int
     split_channel(a, t, cl, v);
     const int c = c0 + cl;
     if (v < n && c < a.C) {
-      const int beg = a.indptr[node0 + v];
-      const int end = a.indptr[node0 + v + 1];
+      // MRP_GRAPH_REGULAR(k): every node has k in-edges, so its CSR row starts at k * node (the
+      // graph kind guarantees it; the host checked) — one dependent load level less
+      const int beg = a.kdeg > 0 ? (node0 + v) * a.kdeg : a.indptr[node0 + v];
+      const int end = a.kdeg > 0 ? beg + a.kdeg : a.indptr[node0 + v + 1];
       const int deg = end - beg;
       float s = 1.f;
       if (BWD && a.mode != MRP_AGG_FILM_SUM && deg > 0) s = 1.f / (float)deg;

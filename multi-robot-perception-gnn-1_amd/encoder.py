@@ -8,7 +8,10 @@
 * ``sigmoid``            — not run here: the aggregation kernels take the logits
   (``MRP_AGG_GB_LOGITS``) and apply it while building their tiles.
 
-The hidden layer's backward (training only) is torch ops; it is not on the forward hot path.
+Backward (training): the two GEMMs of the second Linear (``dh = dz W2`` and ``dW2 = dz^T h``) run
+concurrently on two streams — each alone fills only part of the chip at E = 1792 — and every small
+reduction (the ReLU mask, ``dW1``, ``db1``, ``db2``) runs in one HIP pass (``mrp_edge_encoder_bwd``)
+instead of five torch launches.
 """
 from __future__ import annotations
 
@@ -58,9 +61,73 @@ class EdgeHiddenFunction(torch.autograd.Function):
         return dpose, dw1, db1
 
 
+_side_streams = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    s = _side_streams.get(dev)
+    if s is None:
+        s = _side_streams[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def encoder_backward_reductions(dz, dh, h, pose):
+    """(db2 (2C,), dw1 (C, 9), db1 (C,)) via ``mrp_edge_encoder_bwd`` (see module docstring)."""
+    E, C = h.shape
+    dev = h.device
+    db2 = torch.empty(2 * C, device=dev)
+    dw1 = torch.empty(C, 9, device=dev)
+    db1 = torch.empty(C, device=dev)
+    lib = _lib.load_library()
+    ws = torch.empty(max(int(lib.mrp_edge_encoder_bwd_workspace(E, C)) // 4, 1), device=dev)
+    with torch.cuda.device(dev):
+        code = lib.mrp_edge_encoder_bwd(_ptr(dz), _ptr(dh), _ptr(h), _ptr(pose), E, C, _ptr(db2), _ptr(dw1),
+                                        _ptr(db1), _ptr(ws), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    _lib.check(code, "mrp_edge_encoder_bwd")
+    return db2, dw1, db1
+
+
+class EdgeEncoderFunction(torch.autograd.Function):
+    """z = relu(pose W1^T + b1) W2^T + b2 (``models.py:146-149`` without the Sigmoid)."""
+
+    @staticmethod
+    def forward(ctx, pose, w1, b1, w2, b2):
+        pose = pose.contiguous().float()
+        h = hidden_forward(pose, w1, b1)
+        z = torch.addmm(b2, h, w2.t())
+        ctx.save_for_backward(pose, w1, w2, h)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        pose, w1, w2, h = ctx.saved_tensors
+        dz = dz.contiguous()
+        need = ctx.needs_input_grad
+        cur = torch.cuda.current_stream(dz.device)
+        dw2 = None
+        if need[3]:
+            side = _side_stream(dz.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):  # dW2 = dz^T h beside dh = dz W2
+                dw2 = dz.t().mm(h)
+            dz.record_stream(side)
+            h.record_stream(side)
+        dh = dz.mm(w2) if (need[0] or need[1] or need[2]) else None
+        if dw2 is not None:
+            cur.wait_stream(_side_stream(dz.device))
+            dw2.record_stream(cur)
+        db2 = dw1 = db1 = None
+        if dh is not None or need[4]:
+            db2, dw1, db1 = encoder_backward_reductions(dz, dh if dh is not None else dz[:, : h.shape[1]], h, pose)
+        dpose = (dh * (h > 0)).mm(w1) if need[0] else None
+        return (dpose, dw1 if need[1] else None, db1 if need[2] else None, dw2,
+                db2 if need[4] else None)
+
+
 def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Tensor:
     """Pre-sigmoid FiLM logits z (E, 2C) from the reference-layout ``nn.Sequential``
     (layers 0 and 2 are the Linears)."""
     l1, l2 = enc_layers[0], enc_layers[2]
-    h = EdgeHiddenFunction.apply(pose, l1.weight, l1.bias)
-    return torch.addmm(l2.bias, h, l2.weight.t())
+    if not pose.is_cuda:
+        raise RuntimeError("mrp_gnn: the edge encoder kernels run only on the GPU; no CPU fallback")
+    return EdgeEncoderFunction.apply(pose, l1.weight, l1.bias, l2.weight, l2.bias)

@@ -20,7 +20,7 @@ def declared_symbols():
     syms = set()
     for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
         text = open(h).read()
-        syms |= set(re.findall(r"^\s*(?:int|const char\*|void)\s+(mrp_\w+)\s*\(", text, re.M))
+        syms |= set(re.findall(r"^\s*(?:int|int64_t|const char\*|void)\s+(mrp_\w+)\s*\(", text, re.M))
     return syms
 
 
@@ -100,3 +100,13 @@ def test_frame_graph_build_validation_without_launch():
 def test_frame_batch_needs_the_gpu():
     with pytest.raises(RuntimeError, match="GPU"):
         m.frame_batch(torch.zeros(2, 4, 7))
+
+
+def test_edge_encoder_bwd_validation_without_launch():
+    lib = m.load_library()
+    assert lib.mrp_edge_encoder_bwd_workspace(1792, 512) == 28 * 12 * 512 * 4  # 64-edge chunks x 12C floats
+    assert lib.mrp_edge_encoder_bwd_workspace(0, 512) == 0
+    assert lib.mrp_edge_encoder_bwd(None, None, None, None, -1, 4, None, None, None, None, None) == HIP_INVALID_VALUE
+    # work to do but a missing input or workspace
+    assert lib.mrp_edge_encoder_bwd(None, None, None, None, 8, 4, None, None, None, None, None) == HIP_INVALID_VALUE
+    assert lib.mrp_edge_encoder_bwd(None, None, None, None, 8, 0, None, None, None, None, None) == 0  # C = 0: no-op
