@@ -55,7 +55,10 @@ int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const 
   if (xcopy != nullptr) vec4 = vec4 && (xcopy_node_stride % 4 == 0) && aligned16(xcopy);
   // 16-byte slices beat 8-byte ones at every measured size (tools/kernel_lab.hip product sweep)
   Geometry g = make_geometry(C, P, vec4 ? 4 : 1, 16, 64, mrp::kMaxChanPerBlock);
-  g.grid = (int64_t)num_graphs * g.ncb;
+  // one slice per lane: the plane is split over ceil(PV / lpc) workgroups
+  const int32_t pv = P / g.vec;
+  const int32_t psplit = (pv + g.lpc - 1) / g.lpc;
+  g.grid = (int64_t)num_graphs * g.ncb * psplit;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
   AggArgs a = {};
   a.x = x;
@@ -77,6 +80,7 @@ int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const 
   a.logits = logits;
   a.xc = xcopy;
   a.xcs = xcopy_node_stride;
+  a.psplit = psplit;
   a.kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
   return dispatch_fwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, static_cast<hipStream_t>(stream));
 }

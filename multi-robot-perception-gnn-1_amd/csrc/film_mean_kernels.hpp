@@ -70,6 +70,7 @@ struct AggArgs {
   int32_t kdeg;    // MRP_GRAPH_REGULAR: every node's in-degree (else 0)
   float* xc;       // forward: optional copy of x (the first half of a concatenation buffer)
   int64_t xcs;     // its node stride
+  int32_t psplit;  // forward: plane segments per (graph, channel block) (0 or 1: whole plane)
 };
 
 __device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
@@ -330,8 +331,18 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   float* degf = Gb + a.cpb * SZ;
   unsigned* emask = reinterpret_cast<unsigned*>(degf + NTP);
 
-  const int b = blockIdx.x / a.ncb;
-  const int cb = blockIdx.x - b * a.ncb;
+  // psplit > 1: the plane is cut into psplit contiguous segments, one workgroup each.  The launcher
+  // picks psplit so that every lane owns ONE slice: many short workgroups stream like a plain
+  // grid-stride copy (178 vs 210 us at the bench size, tools/fwd_lab.hip), and the prologue they
+  // repeat is a few KiB of gamma/beta from L2.
+  const int ps = a.psplit > 1 ? a.psplit : 1;
+  const int item = blockIdx.x / ps;
+  const int seg = blockIdx.x - item * ps;
+  const int b = item / a.ncb;
+  const int cb = item - b * a.ncb;
+  const int seglen = (a.PV + ps - 1) / ps;
+  const int jbeg = seg * seglen;
+  const int jend = min(a.PV, jbeg + seglen);
   const int node0 = COMPLETE ? b * NT : a.goff[b];
   const int n = COMPLETE ? NT : min(a.goff[b + 1] - node0, NT);
   if (n <= 0) return;  // whole workgroup: empty graph
@@ -349,9 +360,9 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   const int64_t ebase = (int64_t)b * NT * (NT - 1);
   if (COMPLETE) complete_fetch<NT>(a, ebase, c0, 0, reg);
   // first slice of the sweep, issued before the weight tiles are needed
-  int j = li;
+  int j = jbeg + li;
   Frag<VEC> xv[NT];
-  if (active && j < a.PV) {
+  if (active && j < jend) {
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
       const int uu = u < n ? u : n - 1;  // clamp (ragged batch); never used for output
@@ -370,7 +381,7 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   const bool film = a.mode != MRP_AGG_COPY_MEAN;
   const bool mean = a.mode != MRP_AGG_FILM_SUM;
 
-  while (j < a.PV) {
+  while (j < jend) {
     const int64_t off = (int64_t)j * VEC;
     // Re-read the tiles from LDS every slice: laundering the tile offset stops the compiler from
     // hoisting all N*N weights into registers (which would cost occupancy or spill).
@@ -423,7 +434,7 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
       }
     }
     j += a.lpc;
-    if (j < a.PV) {
+    if (j < jend) {
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         const int uu = u < n ? u : n - 1;
