@@ -62,7 +62,9 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
     g = vec == 2 ? make_geometry(C, P, 2, 16, 16, mrp::kMaxChanPerBlock)
                  : make_geometry(C, P, 1, 32, 32, mrp::kMaxChanPerBlock);
   } else if (max_nodes <= 8) {
-    g = make_geometry(C, P, vec, 8, 64, 32);  // film_bwd_fused
+    // film_bwd_fused: up to 128 lanes (two waves) per plane, two slices per lane: 283 vs 306 us at
+    // 64 lanes at the bench size (tools/fwd_lab.hip backward sweep; 256 lanes: 297 us)
+    g = make_geometry(C, P, vec, 8, 128, 32);
   } else {
     g = make_geometry(C, P, vec, 64, 64, mrp::kMaxChanPerBlock);  // film_bwd_dx + Gram pass
   }

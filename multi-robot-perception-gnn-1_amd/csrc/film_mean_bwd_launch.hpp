@@ -8,7 +8,7 @@ template <int NT, bool COMPLETE, bool DXB>
 hipError_t launch_bwd_ntb(const AggArgs& a_in, const Geometry& g, hipStream_t st) {
   if constexpr (NT <= 8) {
     const AggArgs& a = a_in;
-    const size_t lds = lds_bwd<NT>(g.cpb, COMPLETE && a.logits);
+    const size_t lds = lds_bwd<NT>(g.cpb, COMPLETE && a.logits, g.lpc);
     if (g.vec == 4)
       MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 4, COMPLETE, DXB>), lds);
     else if (g.vec == 2)

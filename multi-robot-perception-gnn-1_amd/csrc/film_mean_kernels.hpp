@@ -62,7 +62,7 @@ struct AggArgs {
   const float* dxb;  // bwd: optional grad_x base (added to grad_x), node stride dxbs
   int64_t dxbs;
   int32_t C, P, PV, mode;
-  int32_t lpc;  // lanes per channel plane (power of two <= 64)
+  int32_t lpc;  // lanes per channel plane (power of two <= 64; <= 256 in film_bwd_fused: lpc/64 waves)
   int32_t cpb;  // channels per workgroup
   int32_t ncb;  // channel blocks per graph
   int32_t want_dx, want_dgb;
@@ -571,10 +571,14 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   constexpr bool kOnePass = VB == NT;
   extern __shared__ float4 smem_f4[];
   float* smem = reinterpret_cast<float*>(smem_f4);
+  // lpc > 64: a channel plane spans wpc = lpc/64 waves (one slice per lane on big planes); each
+  // wave reduces its own Gram partial and the epilogue adds the wpc partials in wave order
+  const int wpc = a.lpc > 64 ? a.lpc >> 6 : 1;
+  const int npg = a.cpb * wpc;   // Gram partials
   float* Wt = smem;              // [cpb][NT][NTP]   scaled, transposed
-  float* Dl = Wt + a.cpb * SZ;   // [cpb][NT][NTP]   Gram (unscaled)
-  float* Sl = Dl + a.cpb * SZ;   // [cpb][NTP]       sum_p G_v
-  float* sc = Sl + a.cpb * NTP;  // [NTP]            s_v
+  float* Dl = Wt + a.cpb * SZ;   // [npg][NT][NTP]   Gram (unscaled)
+  float* Sl = Dl + npg * SZ;     // [npg][NTP]       sum_p G_v
+  float* sc = Sl + npg * NTP;    // [NTP]            s_v
   // COMPLETE with logits: sigmoid(z) of every slot, (cpb x NT x NT) float2 in complete_fetch order,
   // so the epilogue's sigmoid backward does not fetch z from HBM a second time
   float2* Sg = (COMPLETE && a.logits) ? reinterpret_cast<float2*>(sc + NTP) : nullptr;
@@ -704,14 +708,15 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
           }
         }
       });
-      if (active && li == 0) {
+      if (active && (wpc > 1 ? (li & 63) : li) == 0) {
+        const int pg = wpc > 1 ? grp * wpc + (li >> 6) : grp;
 #pragma unroll
         for (int i = 0; i < VB; ++i) {
           const int v = vb + i;
           if (v < NT) {
-            Sl[grp * NTP + v] = S[i];
+            Sl[pg * NTP + v] = S[i];
 #pragma unroll
-            for (int u = 0; u < NT; ++u) Dl[grp * SZ + v * NTP + u] = D[i][u];
+            for (int u = 0; u < NT; ++u) Dl[pg * SZ + v * NTP + u] = D[i][u];
           }
         }
       }
@@ -729,7 +734,12 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
       const int v = slot / NT, u = slot - v * NT;
       const int cc = c0 + cl;
       if (u == v || cc >= a.C) continue;
-      float2 r = make_float2(s * Dl[cl * SZ + v * NTP + u], s * Sl[cl * NTP + v]);
+      float dd = Dl[cl * wpc * SZ + v * NTP + u], ss = Sl[cl * wpc * NTP + v];
+      for (int w = 1; w < wpc; ++w) {
+        dd += Dl[(cl * wpc + w) * SZ + v * NTP + u];
+        ss += Sl[(cl * wpc + w) * NTP + v];
+      }
+      float2 r = make_float2(s * dd, s * ss);
       const int64_t off = (complete_eid(ebase, NT, u, v) * a.C + cc) * 2;
       if (a.logits) {
         // d z = d(gamma, beta) * sig * (1 - sig), sig = sigmoid(z) kept from the prologue
@@ -751,12 +761,16 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
     const int beg = a.indptr[node0 + v];
     const int end = a.indptr[node0 + v + 1];
     const float s = sc[v];
-    const float dbeta = s * Sl[cl * NTP + v];
+    float ss = Sl[cl * wpc * NTP + v];
+    for (int w = 1; w < wpc; ++w) ss += Sl[(cl * wpc + w) * NTP + v];
+    const float dbeta = s * ss;
     for (int k = beg; k < end; ++k) {
       const int u = a.src[k] - node0;
       float dgam = 0.f, dbet = 0.f;
       if ((unsigned)u < (unsigned)n) {
-        dgam = s * Dl[cl * SZ + v * NTP + u];
+        float dd = Dl[cl * wpc * SZ + v * NTP + u];
+        for (int w = 1; w < wpc; ++w) dd += Dl[(cl * wpc + w) * SZ + v * NTP + u];
+        dgam = s * dd;
         dbet = dbeta;
       }
       const int64_t off = ((int64_t)a.eid[k] * a.C + cc) * 2;
@@ -982,9 +996,12 @@ size_t lds_regular(int cpb) {
          2 * (size_t)NT * KMAX * sizeof(int);
 }
 template <int NT>
-size_t lds_bwd(int cpb, bool complete_logits) {
-  // + the per-slot sigmoid values (float2) the COMPLETE epilogue reuses
-  return (size_t)(2 * cpb * mrp::Tile<NT>::SZ + cpb * mrp::Tile<NT>::NTP + mrp::Tile<NT>::NTP) * sizeof(float) +
+size_t lds_bwd(int cpb, bool complete_logits, int lpc = 64) {
+  // + the per-slot sigmoid values (float2) the COMPLETE epilogue reuses; one Gram partial per channel
+  // group, or per wave when a plane spans several waves (lpc > 64)
+  const int npg = lpc > 64 ? cpb * (lpc >> 6) : cpb;
+  return (size_t)(cpb * mrp::Tile<NT>::SZ + npg * mrp::Tile<NT>::SZ + npg * mrp::Tile<NT>::NTP +
+                  mrp::Tile<NT>::NTP) * sizeof(float) +
          (complete_logits ? (size_t)cpb * NT * NT * sizeof(float2) : 0);
 }
 

@@ -130,6 +130,29 @@ def test_backward_vs_oracle(cuda_device, n, hw):
     assert rel_err(gbd.grad.cpu().numpy(), dgb_ref.numpy()) <= TOL
 
 
+@pytest.mark.parametrize("n,bnn", [(3, [3, 3]), (8, [8, 8]), (8, [8, 5, 1]), (12, [12, 12])])
+@pytest.mark.parametrize("hw", [(33, 33), (48, 48), (20, 20), (64, 64), (16, 16)])
+def test_plane_split_geometries(cuda_device, n, bnn, hw):
+    """Large and odd planes: the forward splits each plane over ceil(PV/lanes) workgroups (segments
+    that do not divide the plane, 1-float slices at 33x33), the fused backward spans a plane over
+    two waves (128 lanes) and adds their Gram partials."""
+    H, W = hw
+    g, x, gb = random_case(n, 6, H, W, seed=7 * n + H, bnn=bnn)
+    src, dst = (t.numpy() for t in g.edges())
+    ref = oracle.film_aggregate(x, gb, src, dst).numpy()
+    out = m.film_mean(x.to(cuda_device), gb.to(cuda_device), g.csr(cuda_device)).cpu().numpy()
+    assert rel_err(out, ref) <= TOL
+    if exact_expected(src, dst, 6 * H * W):
+        assert np.array_equal(out, ref)
+    G = torch.randn_like(x)
+    dx_ref, dgb_ref = oracle.film_aggregate_grads(x, gb, src, dst, G)
+    xd = x.to(cuda_device).requires_grad_(True)
+    gbd = gb.to(cuda_device).requires_grad_(True)
+    m.film_mean(xd, gbd, g.csr(cuda_device)).backward(G.to(cuda_device))
+    assert rel_err(xd.grad.cpu().numpy(), dx_ref.numpy()) <= TOL
+    assert rel_err(gbd.grad.cpu().numpy(), dgb_ref.numpy()) <= TOL
+
+
 @pytest.mark.parametrize("knn", [1, 4, 7])
 def test_knn_graphs(cuda_device, knn):
     g, x, gb = random_case(16, 16, 16, 16, seed=knn, knn=knn, bnn=[16, 16, 12])
