@@ -380,6 +380,17 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
 
   const bool film = a.mode != MRP_AGG_COPY_MEAN;
   const bool mean = a.mode != MRP_AGG_FILM_SUM;
+  // CSR: neighbour masks and in-degrees are channel-independent -> wave-uniform; read them from LDS
+  // once into scalar registers instead of once per slice
+  unsigned emv[COMPLETE ? 1 : NT];
+  float degv[COMPLETE ? 1 : NT];
+  if constexpr (!COMPLETE) {
+#pragma unroll
+    for (int v = 0; v < NT; ++v) {
+      emv[v] = __builtin_amdgcn_readfirstlane(emask[v]);
+      degv[v] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, degf[v])));
+    }
+  }
 
   while (j < jend) {
     const int64_t off = (int64_t)j * VEC;
@@ -393,13 +404,17 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
     for (int v = 0; v < NT; ++v) {
       if (!COMPLETE && v >= n) break;
       // neighbour mask of v: compile-time for COMPLETE, else channel-independent -> wave-uniform
-      const unsigned em =
-          COMPLETE ? (((1u << NT) - 1u) & ~(1u << v)) : __builtin_amdgcn_readfirstlane(emask[v]);
+      unsigned em;
+      if constexpr (COMPLETE)
+        em = ((1u << NT) - 1u) & ~(1u << v);
+      else
+        em = emv[v];
       Frag<VEC> acc;
 #pragma unroll
       for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
 #pragma unroll
       for (int u4 = 0; u4 < NTP; u4 += 4) {
+        if (!COMPLETE && ((em >> u4) & 15u) == 0u) continue;  // no neighbour in this quad: skip its LDS reads
         const f4 wa = *reinterpret_cast<const f4*>(A + v * NTP + u4);
         const f4 wb = *reinterpret_cast<const f4*>(Bt + v * NTP + u4);
 #pragma unroll
@@ -416,7 +431,11 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
           }
         }
       }
-      const float d = COMPLETE ? (float)(NT - 1) : degf[v];
+      float d;
+      if constexpr (COMPLETE)
+        d = (float)(NT - 1);
+      else
+        d = degv[v];
       if (mean && d > 0.f) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc.v[k] = acc.v[k] / d;

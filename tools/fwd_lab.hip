@@ -117,6 +117,15 @@ int main(int argc, char** argv) {
     CK((hipError_t)mrp_film_mean_fwd(x, (int64_t)C * P, gb, nullptr, nullptr, nullptr, nullptr, B, N, MRP_GRAPH_COMPLETE, Nt, E, C, P,
                           MRP_AGG_FILM_MEAN | MRP_AGG_GB_LOGITS, out, (int64_t)C * P, nullptr));
   }, iters), alg);
+  {
+    float* cat;
+    CK(hipMalloc(&cat, feat * 8));
+    report("product mrp_film_mean_cat_fwd (x + agg)", time_ms([&] {
+      CK((hipError_t)mrp_film_mean_cat_fwd(x, (int64_t)C * P, gb, nullptr, nullptr, nullptr, nullptr, B, N, MRP_GRAPH_COMPLETE, Nt, E, C, P,
+                                MRP_AGG_FILM_MEAN | MRP_AGG_GB_LOGITS, cat, 2 * (int64_t)C * P, nullptr));
+    }, iters), alg + (double)feat * 4);
+    CK(hipFree(cat));
+  }
   for (int cpb : {4, 2}) {
     if (bwd_only) break;
     for (int ps : {1, 2, 4, 8}) {
