@@ -92,7 +92,7 @@ extern "C" int mrp_edge_hidden_fwd(const float* pose, const float* w1, const flo
 // ---------------------------------------------------------------------------------------------
 namespace mrp_enc {
 
-constexpr int kRows = 64;  // edges per chunk
+constexpr int kRows = 16;  // edges per chunk: 672 workgroups at E = 1792, C = 512 (64 rows: 168 workgroups, 24 us; 16 rows: 7.4 us)
 
 // workspace row per chunk: [0, 2C) db2 partials, then per hidden unit k: 9 dw1 + 1 db1 partials
 __global__ void __launch_bounds__(256) encoder_bwd_partial(const float* __restrict__ dz, const float* __restrict__ dh,
@@ -105,6 +105,7 @@ __global__ void __launch_bounds__(256) encoder_bwd_partial(const float* __restri
   float* out = ws + (int64_t)chunk * 12 * C;
   if (col < 2 * C) {
     float acc = 0.f;
+#pragma unroll 4
     for (int e = e0; e < e1; ++e) acc += dz[(int64_t)e * 2 * C + col];
     out[col] = acc;
   } else if (col < 3 * C) {
@@ -112,6 +113,7 @@ __global__ void __launch_bounds__(256) encoder_bwd_partial(const float* __restri
     float acc[NIN + 1];
 #pragma unroll
     for (int i = 0; i <= NIN; ++i) acc[i] = 0.f;
+#pragma unroll 4
     for (int e = e0; e < e1; ++e) {
       const float g = dh[(int64_t)e * C + k];
       const float d = h[(int64_t)e * C + k] > 0.f ? g : 0.f;
@@ -124,13 +126,27 @@ __global__ void __launch_bounds__(256) encoder_bwd_partial(const float* __restri
   }
 }
 
+// 16 outputs x 16 chunk segments per workgroup (12C/16 workgroups: 384 at C = 512); each segment's
+// partial goes through LDS and segment 0 adds them in segment order (deterministic)
 __global__ void __launch_bounds__(256) encoder_bwd_final(const float* __restrict__ ws, int nchunks, int C,
                                                          float* __restrict__ db2, float* __restrict__ dw1,
                                                          float* __restrict__ db1) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 12 * C) return;
+  __shared__ float part[16][16];
+  const int o = threadIdx.x & 15, sg = threadIdx.x >> 4;
+  const int t = blockIdx.x * 16 + o;
+  const int per = (nchunks + 15) / 16;
+  const int c0 = sg * per, c1 = min(nchunks, c0 + per);
   float acc = 0.f;
-  for (int c = 0; c < nchunks; ++c) acc += ws[(int64_t)c * 12 * C + t];
+  if (t < 12 * C) {
+#pragma unroll 4
+    for (int c = c0; c < c1; ++c) acc += ws[(int64_t)c * 12 * C + t];
+  }
+  part[sg][o] = acc;
+  __syncthreads();
+  if (sg != 0 || t >= 12 * C) return;
+  acc = part[0][o];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) acc += part[k][o];
   if (t < 2 * C) {
     if (db2) db2[t] = acc;
   } else {
@@ -172,7 +188,7 @@ extern "C" int mrp_edge_encoder_bwd(const float* dz, const float* dh, const floa
                      pose, num_edges, C, workspace);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(mrp_enc::encoder_bwd_final, dim3((12 * C + 255) / 256), dim3(256), 0, st, workspace, nchunks, C,
+  hipLaunchKernelGGL(mrp_enc::encoder_bwd_final, dim3((12 * C + 15) / 16), dim3(256), 0, st, workspace, nchunks, C,
                      db2, dw1, db1);
   return hipGetLastError();
 }
