@@ -104,7 +104,7 @@ def test_frame_batch_needs_the_gpu():
 
 def test_edge_encoder_bwd_validation_without_launch():
     lib = m.load_library()
-    assert lib.mrp_edge_encoder_bwd_workspace(1792, 512) == 28 * 12 * 512 * 4  # 64-edge chunks x 12C floats
+    assert lib.mrp_edge_encoder_bwd_workspace(1792, 512) == 112 * 12 * 512 * 4  # 16-edge chunks x 12C floats
     assert lib.mrp_edge_encoder_bwd_workspace(0, 512) == 0
     assert lib.mrp_edge_encoder_bwd(None, None, None, None, -1, 4, None, None, None, None, None) == HIP_INVALID_VALUE
     # work to do but a missing input or workspace
