@@ -230,6 +230,8 @@ def main():
     ap.add_argument("--channels", type=int, default=512)
     ap.add_argument("--hw", type=int, default=32)
     ap.add_argument("--kernel-iters", type=int, default=50)
+    ap.add_argument("--spinup-s", type=float, default=0.5,
+                    help="untimed back-to-back steps before the warmup steps (GPU clock ramp from idle)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample-graphs", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -265,6 +267,17 @@ def main():
         return gcn(g, x)
 
     with torch.no_grad():
+        # Clock / memory power-state ramp: from idle the first ~20-100 ms of back-to-back launches
+        # run up to 1.9x slower (tools/exp_ramp.py: 348 -> 209 -> 188 -> 180 us per aggregation over
+        # the first 60 ms; steps 294 -> 243 -> 226 -> 214 -> 207 us).  Run the step untimed for
+        # --spinup-s seconds first so the K timed steps measure the steady state, not the ramp.
+        spin_t0 = time.perf_counter()
+        spin_steps = 0
+        while time.perf_counter() - spin_t0 < args.spinup_s:
+            for _ in range(20):
+                step()
+            torch.cuda.synchronize(device)
+            spin_steps += 20
         for _ in range(args.warmup):
             step()
         if world > 1:
@@ -303,6 +316,8 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "spinup": {"seconds": args.spinup_s, "steps": spin_steps,
+                   "why": "untimed steps before the warmup so the timed steps see steady GPU clocks"},
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",

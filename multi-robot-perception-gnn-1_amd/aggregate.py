@@ -119,9 +119,10 @@ def film_mean_backward(grad_out: torch.Tensor, x: torch.Tensor, gb: Optional[tor
     if need_dgb and (mode & ~_lib.GB_LOGITS) != _lib.MODE_COPY_MEAN:
         x, xs = _as_node_major(x)
     if gb is not None:
+        # the kernel reads fp32 (gamma, beta) pairs: the same conversion as the forward
         gb = gb.reshape(csr.num_edges, C, 2)
-        if not gb.is_contiguous():
-            gb = gb.contiguous()
+        if not gb.is_contiguous() or gb.dtype != torch.float32:
+            gb = gb.contiguous().float()
     lib = _lib.load_library()
     with torch.cuda.device(x.device):
         code = lib.mrp_film_mean_bwd(
@@ -153,7 +154,7 @@ class FilmMeanFunction(torch.autograd.Function):
         need_dgb = gb is not None and ctx.needs_input_grad[1]
         dx, dgb = film_mean_backward(grad_out, x, gb, ctx.csr, ctx.mode, need_dx, need_dgb)
         if dgb is not None:
-            dgb = dgb.view(gb.shape)
+            dgb = dgb.view(gb.shape).to(gb.dtype)
         return dx, dgb, None, None
 
 
@@ -203,7 +204,7 @@ class FilmMeanCatFunction(torch.autograd.Function):
         dx, dgb = film_mean_backward(grad_buf[:, C:], x, gb, ctx.csr, ctx.mode, need_dx, need_dgb,
                                      grad_x_base=grad_buf[:, :C] if need_dx else None)
         if dgb is not None:
-            dgb = dgb.view(gb.shape)
+            dgb = dgb.view(gb.shape).to(gb.dtype)
         return dx, dgb, None, None
 
 

@@ -202,11 +202,22 @@ def uninstall(saved: dict) -> None:
 
 
 @contextlib.contextmanager
-def reference_class_path(fallback: Optional[types.ModuleType] = None, dgl: bool = True):
+def reference_class_path(fallback: Optional[types.ModuleType] = None, dgl: bool = True,
+                         gcn_return: str = "input"):
     """``with reference_class_path(): ckpt = torch.load(path, weights_only=False)`` — unpickle a
-    reference checkpoint into the MI355X classes."""
+    reference checkpoint into the MI355X classes.
+
+    A reference ``opt`` carries no ``gcn_return``; GCN layers unpickled here without one return
+    ``gcn_return`` — by default ``'input'``, what the reference's ``GCN.forward`` returns
+    (``models.py:226``), so the checkpoint's eval outputs are reproduced.  Pass
+    ``gcn_return='aggregate'`` for the message-passing result (what the scratch variants return)."""
+    if gcn_return not in ("input", "aggregate"):
+        raise ValueError(f"gcn_return must be 'input' or 'aggregate', got {gcn_return!r}")
     saved = install(fallback, dgl)
+    prev = _models.UNPICKLED_GCN_RETURN
+    _models.UNPICKLED_GCN_RETURN = gcn_return
     try:
         yield sys.modules["model.models"]
     finally:
+        _models.UNPICKLED_GCN_RETURN = prev
         uninstall(saved)

@@ -14,6 +14,15 @@ reference's only parallelism (single process, and it cannot scatter a DGLGraph).
   large enough that each ring step over one ~153 GB/s xGMI link is bandwidth- rather than
   latency-bound, few enough that the per-layer edge-encoder (2C^2+12C) and 1x1 compress
   (2C^2+C) gradients of a GCN layer land in one or two buckets.
+
+Averaging: each rank's loss is normally a mean over its own graphs, so with uneven shards
+(``shard_range`` of B graphs over P ranks when P does not divide B) the full-batch gradient is
+``sum_r (n_r / N) g_r``, not ``(1/P) sum_r g_r``.  :meth:`GradAllReducer.set_local_count` gives the
+reducer ``n_r`` (one tiny all-reduce finds ``N``); every bucket is then scaled by ``n_r / N``
+before its SUM all-reduce.  Without it the reducer assumes equal shards and scales by ``1/P``.
+One backward per :meth:`GradAllReducer.synchronize`: a gradient that lands again after its
+bucket's all-reduce was launched (gradient accumulation over several backwards) raises instead
+of silently reducing a partial sum.
 """
 from __future__ import annotations
 
@@ -47,6 +56,31 @@ def shard(items, rank: int, world: int):
     return items[lo:hi]
 
 
+def shard_graph(g, rank: int, world: int):
+    """This rank's share of a batched graph (``dgl.batch`` of frames): the contiguous range of
+    graphs ``shard_range(g.batch_size, rank, world)`` as a batched graph of its own (node and edge
+    ids renumbered from 0, every node/edge feature sliced without a copy).  Returns
+    ``(sub_graph, (lo, hi))``.  Replaces what ``DataParallel`` (``dgl/training.py:324-325``) could
+    not do: scatter a graph batch."""
+    import numpy as np
+
+    from .graph import RobotGraph
+    lo, hi = shard_range(g.batch_size, rank, world)
+    bnn = [int(v) for v in g.batch_num_nodes().tolist()]
+    bne = [int(v) for v in g.batch_num_edges().tolist()]
+    noff = np.concatenate([[0], np.cumsum(bnn)]).astype(np.int64)
+    eoff = np.concatenate([[0], np.cumsum(bne)]).astype(np.int64)
+    n0, n1, e0, e1 = (int(v) for v in (noff[lo], noff[hi], eoff[lo], eoff[hi]))
+    src, dst = g.edges()
+    sub = RobotGraph(src[e0:e1] - n0, dst[e0:e1] - n0, num_nodes=n1 - n0, batch_num_nodes=bnn[lo:hi],
+                     batch_num_edges=bne[lo:hi])
+    for k, v in g.ndata.items():
+        sub.ndata[k] = v[n0:n1]
+    for k, v in g.edata.items():
+        sub.edata[k] = v[e0:e1]
+    return sub, (lo, hi)
+
+
 class GradAllReducer:
     """Bucketed, backward-overlapped gradient averaging over a process group."""
 
@@ -70,11 +104,25 @@ class GradAllReducer:
         for bi, b in enumerate(self.buckets):
             for p in b:
                 self._bucket_of[id(p)] = bi
-        self._pending = [0] * len(self.buckets)
-        self._work = [None] * len(self.buckets)
-        self._flat = [None] * len(self.buckets)
+        self._scale = 1.0 / self.world
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
         self.reset()
+
+    def set_local_count(self, n_local: int) -> float:
+        """This rank holds ``n_local`` of the step's graphs (its loss a mean over them): scale its
+        gradients by ``n_local / N`` (N = the sum over ranks) so the reduced gradient is the
+        full-batch mean even for uneven shards.  Call before backward; returns the scale."""
+        t = torch.tensor([float(n_local)], dtype=torch.float64,
+                         device=self._device() if dist.get_backend(self.group) == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        total = float(t.item())
+        self._scale = float(n_local) / total if total > 0 else 0.0
+        return self._scale
+
+    def _device(self):
+        for b in self.buckets:
+            return b[0].device
+        return torch.device("cpu")
 
     def reset(self) -> None:
         self._pending = [len(b) for b in self.buckets]
@@ -83,6 +131,10 @@ class GradAllReducer:
 
     def _on_grad(self, p: torch.Tensor) -> None:
         bi = self._bucket_of[id(p)]
+        if self._work[bi] is not None:
+            raise RuntimeError("GradAllReducer: a gradient landed after its bucket's all-reduce was launched "
+                               "(more than one backward before synchronize()); call synchronize() after "
+                               "every backward")
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._launch(bi)
@@ -90,6 +142,7 @@ class GradAllReducer:
     def _launch(self, bi: int) -> None:
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.buckets[bi]]
         flat = torch.cat([g.reshape(-1) for g in grads])
+        flat.mul_(self._scale)  # n_r / N (or 1 / P): the SUM all-reduce then yields the average
         self._flat[bi] = flat
         self._work[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
@@ -101,7 +154,7 @@ class GradAllReducer:
                 self._launch(bi)
         for bi, b in enumerate(self.buckets):
             self._work[bi].wait()
-            flat = self._flat[bi].div_(self.world)
+            flat = self._flat[bi]
             off = 0
             for p in b:
                 n = p.numel()

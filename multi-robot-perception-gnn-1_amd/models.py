@@ -25,6 +25,8 @@ Semantics switch ``opt.gcn_return``:
 """
 from __future__ import annotations
 
+import warnings
+
 import torch
 import torch.nn as nn
 
@@ -70,6 +72,11 @@ def _opt(opt, name, default):
     return getattr(opt, name, default) if opt is not None else default
 
 
+#: ``gcn_return`` given to a GCN unpickled from a reference checkpoint whose ``opt`` has none (see
+#: :meth:`GCN.__setstate__`); ``compat.reference_class_path(gcn_return=...)`` sets it.
+UNPICKLED_GCN_RETURN = "input"
+
+
 class GCN(nn.Module):
     """FiLM-mean graph convolution over per-frame robot graphs, ``dgl/model/models.py:213-226``."""
 
@@ -78,9 +85,26 @@ class GCN(nn.Module):
         self.opt = opt
         self.edge_encoder = edge_encoder(layers_dim=[opt.feature_dim, opt.feature_dim])
 
+    def __setstate__(self, state):
+        """Unpickling a checkpoint the reference wrote (``torch.save({'model': model})``,
+        ``dgl/training.py:345-355``): its ``opt`` has no ``gcn_return``, and the reference forward
+        it was trained and evaluated with returns its input (``models.py:226``).  Keep that
+        behaviour so ``eval.py`` reproduces the reference's outputs, and say so once."""
+        super().__setstate__(state)
+        if self.__dict__.get("opt") is not None and not hasattr(self.opt, "gcn_return") \
+                and "gcn_return_default" not in self.__dict__:
+            self.gcn_return_default = UNPICKLED_GCN_RETURN
+            if UNPICKLED_GCN_RETURN == "input":
+                warnings.warn("mrp_gnn: GCN unpickled from a checkpoint without opt.gcn_return: returning the "
+                              "input as the reference's GCN.forward does (models.py:226); set "
+                              "opt.gcn_return='aggregate' for the message-passing result", stacklevel=2)
+
+    def _return_mode(self) -> str:
+        return _opt(self.opt, "gcn_return", self.__dict__.get("gcn_return_default", "aggregate"))
+
     def forward(self, g, feats: torch.Tensor = None) -> torch.Tensor:
         x = g.ndata["image"] if feats is None else feats
-        if _opt(self.opt, "gcn_return", "aggregate") == "input":
+        if self._return_mode() == "input":
             return x  # models.py:226 returns the input; update_all's result is never read
         mode = _opt(self.opt, "gcn_mode", "film_mean")
         if mode == "copy_mean":
@@ -93,7 +117,7 @@ class GCN(nn.Module):
         """``torch.cat((feats, self(g, feats)), 1)`` (``models.py:181-182``) with the aggregate written
         straight into the concatenation buffer (and the backward fused likewise)."""
         x = g.ndata["image"] if feats is None else feats
-        if _opt(self.opt, "gcn_return", "aggregate") == "input" or not x.is_cuda:
+        if self._return_mode() == "input" or not x.is_cuda:
             return torch.cat((x, self(g, x)), dim=1)
         mode = _opt(self.opt, "gcn_mode", "film_mean")
         if mode == "copy_mean":

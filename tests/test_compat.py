@@ -20,7 +20,9 @@ CKPT = os.path.join(GOLDEN_DIR, "ref_gcn_checkpoint.pt")
 
 
 def load_reference_checkpoint(**kw):
-    with m.compat.reference_class_path(**kw):
+    import warnings
+    with m.compat.reference_class_path(**kw), warnings.catch_warnings():
+        warnings.simplefilter("ignore")
         return torch.load(CKPT, weights_only=False)
 
 
@@ -39,6 +41,21 @@ def test_reference_checkpoint_unpickles_into_native_classes():
     stack = ck["stack"]
     assert type(stack.gcn2) is m.GCN and stack.gcn1 is gcn
     assert gcn.opt.feature_dim == 8 and gcn.opt.compress_gcn  # the reference's argparse opt travels along
+    # the reference opt has no gcn_return: the unpickled layers keep the reference's return-the-input
+    assert not hasattr(gcn.opt, "gcn_return") and gcn.gcn_return_default == "input"
+    assert load_reference_checkpoint(gcn_return="aggregate")["model"].gcn_return_default == "aggregate"
+
+
+def test_unpickled_reference_gcn_warns_and_returns_input():
+    with m.compat.reference_class_path():
+        with pytest.warns(UserWarning, match="models.py:226"):
+            ck = torch.load(CKPT, weights_only=False)
+    io = load_golden("ref_gcn_checkpoint_io")
+    g = m.RobotGraph(io["src"], io["dst"], num_nodes=io["x"].shape[0], batch_num_nodes=[4, 4],
+                     batch_num_edges=[12, 12])
+    x = torch.from_numpy(io["x"])
+    g.ndata["image"] = x
+    assert ck["model"](g) is x  # what the reference forward returns; no kernel runs (works on the CPU)
 
 
 def test_models_alias_resolves_reference_only_names_through_fallback():
@@ -88,6 +105,9 @@ def test_reference_checkpoint_runs_on_the_hip_path(cuda_device):
     g.edata["pose"] = torch.from_numpy(io["pose"])
     gd = g.to(cuda_device)
     stack = ck["stack"].to(cuda_device)
+    with torch.no_grad():
+        assert stack.gcn1(gd) is gd.ndata["image"]  # the reference as shipped returns its input
+    stack = load_reference_checkpoint(gcn_return="aggregate")["stack"].to(cuda_device)
     with torch.no_grad():
         assert rel_err(stack.gcn1(gd).cpu(), io["out_gcn1"]) <= 1e-5
         assert rel_err(stack.gcn2(gd).cpu(), io["out_gcn2"]) <= 1e-5

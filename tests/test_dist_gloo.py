@@ -64,3 +64,94 @@ def _worker(rank, world, port, bucket_bytes):
 @pytest.mark.parametrize("bucket_bytes", [256, 32 << 20])
 def test_grad_allreduce_world2_matches_full_batch(bucket_bytes):
     mp.spawn(_worker, args=(2, _free_port(), bucket_bytes), nprocs=2, join=True)
+
+
+def _gcn_params(C):
+    torch.manual_seed(5)
+    import mrp_gnn_amd as m
+    opt = type("opt", (), {"feature_dim": C, "compress_gcn": True, "multi_gcn": False})()
+    blk = m.GCNBlock(opt)
+    return {k: v.detach().clone() for k, v in blk.named_parameters()}
+
+
+def _block_loss(params, g):
+    """mean((conv1(cat(x, gcn1(x))))^2) with the CPU oracle for the GCN layer
+    (dgl/model/models.py:180-184): the edge encoder and conv1 parameters are the leaves."""
+    import oracle
+    enc = {k[len("gcn1.edge_encoder."):]: v for k, v in params.items() if k.startswith("gcn1.edge_encoder.")}
+    x = g.ndata["image"]
+    src, dst = (t.numpy() for t in g.edges())
+    agg = oracle.film_aggregate(x, oracle.edge_encoder_forward(enc, g.edata["pose"]), src, dst)
+    h = torch.nn.functional.conv2d(torch.cat((x, agg), 1), params["conv1.weight"], params["conv1.bias"])
+    return h.square().mean()
+
+
+def _frames(B, N, C, seed):
+    import numpy as np
+
+    import mrp_gnn_amd as m
+    rng = np.random.RandomState(seed)
+    frames = []
+    for _ in range(B):
+        poses = np.concatenate([rng.uniform(-5, 5, (N, 3)), rng.standard_normal((N, 4))], 1).astype(np.float32)
+        f = m.frame_graph(poses)
+        f.ndata["image"] = torch.from_numpy(rng.standard_normal((N, C, 4, 4)).astype(np.float32))
+        frames.append(f)
+    return m.batch(frames)
+
+
+def _gcn_worker(rank, world, port, B):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mrp_gnn_amd.dist import shard_graph
+        C = 8
+        g = _frames(B, 4, C, seed=11)
+        # full batch on one process: the reference gradient
+        ref = {k: v.clone().requires_grad_(True) for k, v in _gcn_params(C).items()}
+        _block_loss(ref, g).backward()
+        # this rank's graphs only, gradients reduced (weighted by graph count: uneven shards)
+        params = {k: torch.nn.Parameter(v.clone()) for k, v in _gcn_params(C).items()}
+        red = GradAllReducer(params.values(), bucket_bytes=4096)
+        sub, (lo, hi) = shard_graph(g, rank, world)
+        assert sub.batch_size == hi - lo and sub.num_nodes() == 4 * (hi - lo)
+        assert torch.equal(sub.ndata["image"], g.ndata["image"][4 * lo:4 * hi])
+        for _ in range(2):
+            for p in params.values():
+                p.grad = None
+            red.set_local_count(hi - lo)
+            _block_loss(params, sub).backward()
+            red.synchronize()
+            for k in params:
+                assert torch.allclose(params[k].grad, ref[k].grad, rtol=1e-5, atol=1e-7), (rank, k)
+        red.remove()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B", [4, 5])
+def test_gcn_layer_grads_world2_sharded_batch(B):
+    """The GCN layer's parameters (edge encoder + 1x1 compress) trained data-parallel over a
+    sharded RobotGraph batch: the reduced gradients equal the full-batch ones, including an
+    uneven split (B=5 over 2 ranks: 3 + 2 graphs)."""
+    mp.spawn(_gcn_worker, args=(2, _free_port(), B), nprocs=2, join=True)
+
+
+def _accum_worker(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model = _model()
+        red = GradAllReducer(model.parameters())
+        data = torch.randn(4, 9)
+        model(data).sum().backward()
+        with pytest.raises(RuntimeError, match="synchronize"):
+            model(data).sum().backward()  # a second backward before synchronize()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_second_backward_before_synchronize_raises():
+    mp.spawn(_accum_worker, args=(2, _free_port()), nprocs=2, join=True)
