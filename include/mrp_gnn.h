@@ -50,7 +50,16 @@ extern "C" {
  * every graph has exactly max_nodes nodes, edges are all ordered pairs u != v, numbered graph by
  * graph in i-major order (edge u->v of graph b is b*n*(n-1) + u*(n-1) + (v < u ? v : v-1)), and
  * node ids are graph by graph.  indptr/src/eid/graph_off are then not read (may be NULL).
- * MRP_GRAPH_CSR is any batch of disjoint graphs described by the CSR arrays. */
+ * MRP_GRAPH_CSR is any batch of disjoint graphs described by the CSR arrays.
+ *
+ * Preconditions the kernels rely on and do not check on the device (the library never reads
+ * device memory on the host; RobotGraph.csr() establishes them, and breaking them gives wrong or
+ * partially unwritten outputs rather than an error):
+ *   - every graph b has graph_off[b+1] - graph_off[b] <= max_nodes nodes;
+ *   - every edge's source lies in its destination's graph;
+ *   - MRP_GRAPH_REGULAR(k): every node has exactly k in-edges, so node v's CSR row is
+ *     [k*v, k*(v+1)) (indptr is then not read by the forward);
+ *   - MRP_GRAPH_COMPLETE: the edge numbering below. */
 enum mrp_graph_kind {
     MRP_GRAPH_CSR = 0,
     MRP_GRAPH_COMPLETE = 1
@@ -145,6 +154,61 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride,
                       void* stream);
 
 /*
+ * Epilogue of the aggregation, for the layer compositions around update_all.  With a = the
+ * aggregate of destination v (as mrp_film_mean_fwd computes it), the forward writes
+ *
+ *   out[v] = agg_scale * a + self_scale * x[v] + x0_scale * x0[v]
+ *
+ * evaluated left to right in fp32 (each product rounded, then each sum; a scale of 1 is exact), and
+ * if xcopy != NULL also stores x[v] at xcopy + v * xcopy_node_stride.  Uses:
+ *   - plain aggregation:  {1, 0, NULL, 0, 0, NULL, 0} (what a NULL epilogue pointer means);
+ *   - residual h = g_h + h (dgl/model/dgl_models.py:36-37): agg_scale 1, self_scale 1 — x[v] is
+ *     already in registers, so this costs no traffic;
+ *   - initial-feature mix (GCN2-style, (1 - alpha) * a + alpha * x0; not in the reference, parity
+ *     unpinned): agg_scale 1 - alpha, x0 = the first layer's input, x0_scale alpha;
+ *   - torch.cat((x, a), 1) (dgl/model/models.py:182): xcopy = the first half of the concatenation
+ *     buffer (mrp_film_mean_cat_fwd is this with out = its second half).
+ * The backward (mrp_film_mean_bwd_ex) reads agg_scale and self_scale: grad_out reaches the
+ * aggregation scaled by agg_scale, and self_scale * grad_out[u] is added to grad_x[u].  The
+ * gradient of x0 is x0_scale * grad_out (an elementwise product the caller forms); x0 and xcopy
+ * are not read by the backward.
+ */
+typedef struct mrp_agg_epilogue {
+    float agg_scale;
+    float self_scale;
+    const float* x0;
+    int64_t x0_node_stride;
+    float x0_scale;
+    float* xcopy;
+    int64_t xcopy_node_stride;
+} mrp_agg_epilogue;
+
+/* mrp_film_mean_fwd with an epilogue (NULL: plain).  x0 and xcopy rows use the node ids of x. */
+int mrp_film_mean_fwd_ex(const float* x, int64_t x_node_stride,
+                         const float* gb,
+                         const int32_t* indptr, const int32_t* src, const int32_t* eid,
+                         const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes,
+                         int32_t graph_kind, int32_t num_nodes, int32_t num_edges,
+                         int32_t C, int32_t P, int32_t mode,
+                         float* out, int64_t out_node_stride,
+                         const mrp_agg_epilogue* epilogue,
+                         void* stream);
+
+/* mrp_film_mean_bwd for a forward run with `epilogue` (NULL: plain; see mrp_agg_epilogue). */
+int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride,
+                         const float* x, int64_t x_node_stride,
+                         const float* gb,
+                         const int32_t* indptr, const int32_t* src, const int32_t* eid,
+                         const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes,
+                         int32_t graph_kind, int32_t num_nodes, int32_t num_edges,
+                         int32_t C, int32_t P, int32_t mode,
+                         float* grad_x, int64_t gx_node_stride,
+                         const float* grad_x_base, int64_t base_node_stride,
+                         float* grad_gb,
+                         const mrp_agg_epilogue* epilogue,
+                         void* stream);
+
+/*
  * First layer of the edge encoder, dgl/model/models.py:147-148:  h = relu(pose W1^T + b1).
  *   pose (num_edges, 9), w1 (C, 9) (nn.Linear weight layout), b1 (C) -> h (num_edges, C), fp32.
  * The second Linear is a plain library GEMM and its Sigmoid is fused into the aggregation
@@ -188,6 +252,11 @@ int mrp_edge_encoder_bwd(const float* dz, const float* dh, const float* h, const
 int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int32_t knn_k,
                           float* edge_pose, int32_t* indptr, int32_t* src, int32_t* eid,
                           int32_t* graph_off, void* stream);
+
+/* Experiment knobs of the launchers (kernel-lab sweeps; not needed for normal use).  Returns
+ * hipErrorInvalidValue for an unknown name.  "fwd_regular_split": 1 (default) splits each channel
+ * plane of a MRP_GRAPH_REGULAR forward over several workgroups, 0 keeps whole planes. */
+int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes). */
 int mrp_abi_version(void);

@@ -22,14 +22,17 @@ EXPORTED_SYMBOLS = (
     "mrp_film_mean_fwd",
     "mrp_film_mean_cat_fwd",
     "mrp_film_mean_bwd",
+    "mrp_film_mean_fwd_ex",
+    "mrp_film_mean_bwd_ex",
     "mrp_edge_hidden_fwd",
     "mrp_edge_encoder_bwd_workspace",
     "mrp_edge_encoder_bwd",
     "mrp_frame_graph_build",
+    "mrp_tuning_set",
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 9
+ABI_VERSION = 10
 MAX_NODES = 16
 
 MODE_FILM_MEAN = 0
@@ -48,6 +51,15 @@ def graph_regular(k: int) -> int:
     return (k << 8) | 2
 MODES = {"film_mean": MODE_FILM_MEAN, "film_sum": MODE_FILM_SUM, "copy_mean": MODE_COPY_MEAN}
 
+class Epilogue(ctypes.Structure):
+    """``mrp_agg_epilogue`` (include/mrp_gnn.h): out = agg_scale*a + self_scale*x[v] + x0_scale*x0[v],
+    plus an optional copy of x[v] (the first half of a concatenation buffer)."""
+
+    _fields_ = [("agg_scale", ctypes.c_float), ("self_scale", ctypes.c_float), ("x0", ctypes.c_void_p),
+                ("x0_node_stride", ctypes.c_int64), ("x0_scale", ctypes.c_float), ("xcopy", ctypes.c_void_p),
+                ("xcopy_node_stride", ctypes.c_int64)]
+
+
 _lock = threading.Lock()
 _lib = None
 
@@ -64,6 +76,13 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_film_mean_cat_fwd.restype = ctypes.c_int
     lib.mrp_film_mean_bwd.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _I64, _P, _P]
     lib.mrp_film_mean_bwd.restype = ctypes.c_int
+    ep = ctypes.POINTER(Epilogue)
+    lib.mrp_film_mean_fwd_ex.argtypes = [_P, _I64, _P] + graph + [_P, _I64, ep, _P]
+    lib.mrp_film_mean_fwd_ex.restype = ctypes.c_int
+    lib.mrp_film_mean_bwd_ex.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _I64, _P, ep, _P]
+    lib.mrp_film_mean_bwd_ex.restype = ctypes.c_int
+    lib.mrp_tuning_set.argtypes = [ctypes.c_char_p, _I32]
+    lib.mrp_tuning_set.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]

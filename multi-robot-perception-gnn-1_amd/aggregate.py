@@ -60,27 +60,73 @@ def _stream(dev: torch.device) -> ctypes.c_void_p:
 
 
 def film_mean_forward_into(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode: int,
-                           out: torch.Tensor) -> torch.Tensor:
+                           out: torch.Tensor, epilogue: Optional["EpilogueSpec"] = None) -> torch.Tensor:
     """Run the forward kernel into ``out`` (N, C, H, W) — which may be a strided view such as
     the second half of a ``torch.cat((h, g_h), 1)`` buffer.  No autograd."""
-    return _forward(x, gb, csr, mode, out, cat=False)
+    return _forward(x, gb, csr, mode, out, epilogue=epilogue)
 
 
 def film_mean_cat_forward_into(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode: int,
                                cat: torch.Tensor) -> torch.Tensor:
     """``cat[:, :C] = x; cat[:, C:] = film_mean(x)`` for a (N, 2C, H, W) buffer, one kernel pass
     (``mrp_film_mean_cat_fwd``).  No autograd."""
-    return _forward(x, gb, csr, mode, cat, cat=True)
+    C = x.shape[1]
+    if cat.dim() != 4 or tuple(cat.shape) != (x.shape[0], 2 * C) + tuple(x.shape[2:]):
+        raise ValueError(f"cat must be {(x.shape[0], 2 * C) + tuple(x.shape[2:])} fp32")
+    return _forward(x, gb, csr, mode, cat[:, C:], epilogue=EpilogueSpec(xcopy=cat[:, :C]))
 
 
-def _forward(x, gb, csr, mode, out, cat):
+class EpilogueSpec:
+    """What the forward writes per destination v (``mrp_agg_epilogue``, include/mrp_gnn.h):
+    ``out[v] = agg_scale * a + self_scale * x[v] + x0_scale * x0[v]``, optionally also ``xcopy[v] = x[v]``.
+
+    * residual ``h = g_h + h`` (``dgl/model/dgl_models.py:36-37``): ``self_scale=1``;
+    * initial-feature mix ``(1 - alpha) a + alpha x0`` (GCN2-style; not in the reference):
+      ``agg_scale=1-alpha, x0=h0, x0_scale=alpha``;
+    * ``torch.cat((x, a), 1)`` (``dgl/model/models.py:182``): ``xcopy`` = the first half."""
+
+    def __init__(self, agg_scale: float = 1.0, self_scale: float = 0.0, x0: Optional[torch.Tensor] = None,
+                 x0_scale: float = 0.0, xcopy: Optional[torch.Tensor] = None):
+        self.agg_scale = float(agg_scale)
+        self.self_scale = float(self_scale)
+        self.x0 = x0
+        self.x0_scale = float(x0_scale)
+        self.xcopy = xcopy
+
+    def is_plain(self) -> bool:
+        return self.agg_scale == 1.0 and self.self_scale == 0.0 and self.x0 is None and self.xcopy is None
+
+
+def _epilogue_struct(ep: Optional[EpilogueSpec], shape):
+    """(ctypes Epilogue or None, tensors to keep alive)."""
+    if ep is None or ep.is_plain():
+        return None, ()
+    keep = []
+    x0p, x0s, xcp, xcs = 0, 0, 0, 0
+    if ep.x0 is not None:
+        if tuple(ep.x0.shape) != tuple(shape):
+            raise ValueError(f"x0 must have the node features' shape {tuple(shape)}")
+        _require_device(ep.x0)
+        x0, x0s = _as_node_major(ep.x0.float() if ep.x0.dtype != torch.float32 else ep.x0)
+        keep.append(x0)
+        x0p = x0.data_ptr()
+    if ep.xcopy is not None:
+        xcs = node_stride(ep.xcopy)
+        if xcs is None or tuple(ep.xcopy.shape) != tuple(shape):
+            raise ValueError("xcopy must be (N, C, H, W) fp32 with a contiguous block per node")
+        _require_device(ep.xcopy)
+        xcp = ep.xcopy.data_ptr()
+    st = _lib.Epilogue(ep.agg_scale, ep.self_scale, x0p, x0s, ep.x0_scale, xcp, xcs)
+    return st, keep
+
+
+def _forward(x, gb, csr, mode, out, epilogue=None):
     _require_device(x, out)
     n, C, H, W = x.shape
     x, xs = _as_node_major(x)
     os_ = node_stride(out)
-    want = (n, 2 * C, H, W) if cat else (n, C, H, W)
-    if os_ is None or tuple(out.shape) != want:
-        raise ValueError(f"out must be {want} fp32 with a contiguous block per node")
+    if os_ is None or tuple(out.shape) != (n, C, H, W):
+        raise ValueError(f"out must be {(n, C, H, W)} fp32 with a contiguous block per node")
     if (mode & ~_lib.GB_LOGITS) != _lib.MODE_COPY_MEAN:
         if gb is None:
             raise ValueError("gamma/beta tensor required for FiLM modes")
@@ -92,21 +138,23 @@ def _forward(x, gb, csr, mode, out, cat):
         gb = None
     if n != csr.num_nodes:
         raise ValueError(f"x has {n} nodes, graph has {csr.num_nodes}")
+    ep, _keep = _epilogue_struct(epilogue, x.shape)
     lib = _lib.load_library()
-    fn = lib.mrp_film_mean_cat_fwd if cat else lib.mrp_film_mean_fwd
     with torch.cuda.device(x.device):
-        code = fn(
+        code = lib.mrp_film_mean_fwd_ex(
             _ptr(x), xs, _ptr(gb), _ptr(csr.indptr), _ptr(csr.src), _ptr(csr.eid), _ptr(csr.graph_off),
             csr.num_graphs, csr.max_nodes, csr.graph_kind, csr.num_nodes, csr.num_edges, C, H * W, mode,
-            _ptr(out), os_, _stream(x.device))
-    _lib.check(code, "mrp_film_mean_cat_fwd" if cat else "mrp_film_mean_fwd")
+            _ptr(out), os_, ctypes.byref(ep) if ep is not None else None, _stream(x.device))
+    _lib.check(code, "mrp_film_mean_fwd_ex")
     return out
 
 
 def film_mean_backward(grad_out: torch.Tensor, x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR,
-                       mode: int, need_dx: bool, need_dgb: bool, grad_x_base: Optional[torch.Tensor] = None):
+                       mode: int, need_dx: bool, need_dgb: bool, grad_x_base: Optional[torch.Tensor] = None,
+                       epilogue: Optional[EpilogueSpec] = None):
     """(grad_x or None, grad_gb (E, C, 2) or None) for the forward above; ``grad_x_base`` (N, C, H, W),
-    if given, is added into grad_x by the kernel."""
+    if given, is added into grad_x by the kernel.  ``epilogue``: the forward's (its agg_scale and
+    self_scale enter here; the gradient of x0 is x0_scale * grad_out, formed by the caller)."""
     _require_device(grad_out, x)
     n, C, H, W = x.shape
     grad_out, gs = _as_node_major(grad_out)
@@ -123,28 +171,36 @@ def film_mean_backward(grad_out: torch.Tensor, x: torch.Tensor, gb: Optional[tor
         gb = gb.reshape(csr.num_edges, C, 2)
         if not gb.is_contiguous() or gb.dtype != torch.float32:
             gb = gb.contiguous().float()
+    ep = None
+    if epilogue is not None and (epilogue.agg_scale != 1.0 or epilogue.self_scale != 0.0):
+        ep = _lib.Epilogue(epilogue.agg_scale, epilogue.self_scale, 0, 0, 0.0, 0, 0)
     lib = _lib.load_library()
     with torch.cuda.device(x.device):
-        code = lib.mrp_film_mean_bwd(
+        code = lib.mrp_film_mean_bwd_ex(
             _ptr(grad_out), gs, _ptr(x), xs, _ptr(gb), _ptr(csr.indptr), _ptr(csr.src), _ptr(csr.eid),
             _ptr(csr.graph_off), csr.num_graphs, csr.max_nodes, csr.graph_kind, csr.num_nodes, csr.num_edges, C,
             H * W, mode,
-            _ptr(dx), (C * H * W) if dx is not None else 0, _ptr(grad_x_base), bs, _ptr(dgb), _stream(x.device))
-    _lib.check(code, "mrp_film_mean_bwd")
+            _ptr(dx), (C * H * W) if dx is not None else 0, _ptr(grad_x_base), bs, _ptr(dgb),
+            ctypes.byref(ep) if ep is not None else None, _stream(x.device))
+    _lib.check(code, "mrp_film_mean_bwd_ex")
     return dx, dgb
 
 
 class FilmMeanFunction(torch.autograd.Function):
-    """Autograd wrapper: forward = ``mrp_film_mean_fwd``, backward = ``mrp_film_mean_bwd``.
-    ``mode`` may carry ``_lib.GB_LOGITS`` (gb = pre-sigmoid logits; the gradient is then d logits)."""
+    """Autograd wrapper: forward = ``mrp_film_mean_fwd_ex``, backward = ``mrp_film_mean_bwd_ex``.
+    ``mode`` may carry ``_lib.GB_LOGITS`` (gb = pre-sigmoid logits; the gradient is then d logits).
+    ``scales`` = (agg_scale, self_scale, x0_scale) of the epilogue (``EpilogueSpec``); x0 may be None."""
 
     @staticmethod
-    def forward(ctx, x, gb, csr: GraphCSR, mode: int):
+    def forward(ctx, x, gb, x0, csr: GraphCSR, mode: int, scales=(1.0, 0.0, 0.0)):
         out = torch.empty(x.shape, device=x.device, dtype=torch.float32)
-        film_mean_forward_into(x, gb, csr, mode, out)
+        ep = EpilogueSpec(scales[0], scales[1], x0, scales[2])
+        film_mean_forward_into(x, gb, csr, mode, out, epilogue=ep)
         ctx.save_for_backward(x, gb)
         ctx.csr = csr
         ctx.mode = mode
+        ctx.scales = scales
+        ctx.x0_dtype = x0.dtype if x0 is not None else None
         return out
 
     @staticmethod
@@ -152,10 +208,29 @@ class FilmMeanFunction(torch.autograd.Function):
         x, gb = ctx.saved_tensors
         need_dx = ctx.needs_input_grad[0]
         need_dgb = gb is not None and ctx.needs_input_grad[1]
-        dx, dgb = film_mean_backward(grad_out, x, gb, ctx.csr, ctx.mode, need_dx, need_dgb)
+        ep = EpilogueSpec(ctx.scales[0], ctx.scales[1])
+        dx, dgb = film_mean_backward(grad_out, x, gb, ctx.csr, ctx.mode, need_dx, need_dgb, epilogue=ep)
         if dgb is not None:
             dgb = dgb.view(gb.shape).to(gb.dtype)
-        return dx, dgb, None, None
+        dx0 = None
+        if ctx.needs_input_grad[2]:
+            dx0 = (grad_out * ctx.scales[2]).to(ctx.x0_dtype)
+        return dx, dgb, dx0, None, None, None
+
+
+def _mode_flags(mode, logits: bool) -> int:
+    m = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
+    if m != _lib.MODE_COPY_MEAN and logits:
+        m |= _lib.GB_LOGITS
+    return m
+
+
+def _check_x(x):
+    if x.dim() != 4:
+        raise ValueError(f"node features must be (N, C, H, W), got {tuple(x.shape)}")
+    if x.dtype != torch.float32:
+        raise TypeError("node features must be float32 (the reference path is fp32)")
+    _require_device(x)
 
 
 def film_mean(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="film_mean",
@@ -166,24 +241,41 @@ def film_mean(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="
     (ignored for ``mode='copy_mean'``), or their pre-sigmoid logits with ``logits=True`` (the
     encoder's Sigmoid then runs inside the kernel); csr: ``RobotGraph.csr(device)``.
     """
-    m = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
-    if x.dim() != 4:
-        raise ValueError(f"node features must be (N, C, H, W), got {tuple(x.shape)}")
-    if x.dtype != torch.float32:
-        raise TypeError("node features must be float32 (the reference path is fp32)")
-    _require_device(x)
-    if m == _lib.MODE_COPY_MEAN:
+    _check_x(x)
+    m = _mode_flags(mode, logits)
+    if (m & ~_lib.GB_LOGITS) == _lib.MODE_COPY_MEAN:
         gb = None
-    elif logits:
-        m |= _lib.GB_LOGITS
-    return FilmMeanFunction.apply(x, gb, csr, m)
+    return FilmMeanFunction.apply(x, gb, None, csr, m)
+
+
+def film_mean_residual(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="film_mean",
+                       logits: bool = False) -> torch.Tensor:
+    """``x + film_mean(x, ...)`` in one pass — the residual combination ``h = g_h + h`` of
+    ``dgl/model/dgl_models.py:36-37`` (x[v] is already in registers: no extra traffic)."""
+    _check_x(x)
+    m = _mode_flags(mode, logits)
+    if (m & ~_lib.GB_LOGITS) == _lib.MODE_COPY_MEAN:
+        gb = None
+    return FilmMeanFunction.apply(x, gb, None, csr, m, (1.0, 1.0, 0.0))
+
+
+def film_mean_mix(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, x0: torch.Tensor, alpha: float,
+                  mode="film_mean", logits: bool = False) -> torch.Tensor:
+    """``(1 - alpha) * film_mean(x, ...) + alpha * x0`` in one pass: the initial-feature mix of a
+    GCN2-style layer (BASELINE configs[3]'s "GCN2Conv"; not in the reference, parity unpinned)."""
+    _check_x(x)
+    m = _mode_flags(mode, logits)
+    if (m & ~_lib.GB_LOGITS) == _lib.MODE_COPY_MEAN:
+        gb = None
+    return FilmMeanFunction.apply(x, gb, x0, csr, m, (1.0 - float(alpha), 0.0, float(alpha)))
 
 
 class FilmMeanCatFunction(torch.autograd.Function):
     """``torch.cat((x, film_mean(x, gb)), 1)`` without the concatenation pass for the aggregate
     (``dgl/model/models.py:181-182,187-188``): the kernel writes the aggregate into the second half of
-    the (N, 2C, H, W) buffer and x, whose slices it holds anyway, into the first; backward hands the kernel the second half of the incoming gradient as
-    grad_out and the first half as the base of x's gradient."""
+    the (N, 2C, H, W) buffer and x, whose slices it holds anyway, into the first; backward hands the
+    kernel the second half of the incoming gradient as grad_out and the first half as the base of
+    x's gradient."""
 
     @staticmethod
     def forward(ctx, x, gb, csr: GraphCSR, mode: int):
@@ -211,12 +303,10 @@ class FilmMeanCatFunction(torch.autograd.Function):
 def film_mean_cat(x: torch.Tensor, gb: Optional[torch.Tensor], csr: GraphCSR, mode="film_mean",
                   logits: bool = False) -> torch.Tensor:
     """``torch.cat((x, film_mean(x, gb, csr, mode, logits)), dim=1)`` in one kernel pass."""
-    m = _lib.MODES[mode] if isinstance(mode, str) else int(mode)
     if x.dim() != 4 or x.dtype != torch.float32:
         raise ValueError("node features must be (N, C, H, W) float32")
     _require_device(x)
-    if m == _lib.MODE_COPY_MEAN:
+    m = _mode_flags(mode, logits)
+    if (m & ~_lib.GB_LOGITS) == _lib.MODE_COPY_MEAN:
         gb = None
-    elif logits:
-        m |= _lib.GB_LOGITS
     return FilmMeanCatFunction.apply(x, gb, csr, m)

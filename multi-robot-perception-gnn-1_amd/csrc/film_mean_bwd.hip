@@ -24,6 +24,19 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
                       int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode_flags, float* grad_x,
                       int64_t gx_node_stride, const float* grad_x_base, int64_t base_node_stride, float* grad_gb,
                       void* stream) {
+  return mrp_film_mean_bwd_ex(grad_out, g_node_stride, x, x_node_stride, gb, indptr, src, eid, graph_off, num_graphs,
+                              max_nodes, graph_kind, num_nodes, num_edges, C, P, mode_flags, grad_x, gx_node_stride,
+                              grad_x_base, base_node_stride, grad_gb, nullptr, stream);
+}
+
+int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const float* x, int64_t x_node_stride,
+                         const float* gb, const int32_t* indptr, const int32_t* src, const int32_t* eid,
+                         const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
+                         int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode_flags,
+                         float* grad_x, int64_t gx_node_stride, const float* grad_x_base, int64_t base_node_stride,
+                         float* grad_gb, const mrp_agg_epilogue* ep, void* stream) {
+  const float agg_scale = ep != nullptr ? ep->agg_scale : 1.f;
+  const float self_scale = ep != nullptr ? ep->self_scale : 0.f;
   const int32_t logits = (mode_flags & MRP_AGG_GB_LOGITS) ? 1 : 0;
   const int32_t mode = mode_flags & ~MRP_AGG_GB_LOGITS;
   if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind, num_nodes, num_edges, C, P,
@@ -31,12 +44,12 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
     return hipErrorInvalidValue;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool copy = mode == MRP_AGG_COPY_MEAN;
-  if (grad_gb != nullptr && num_edges > 0 && C > 0 && (copy || num_nodes == 0 || P == 0)) {
+  if (grad_gb != nullptr && num_edges > 0 && C > 0 && (copy || num_nodes == 0 || P == 0 || agg_scale == 0.f)) {
     // gamma/beta do not influence the output: their gradient is zero.
     hipError_t e = hipMemsetAsync(grad_gb, 0, (size_t)num_edges * C * 2 * sizeof(float), st);
     if (e != hipSuccess) return e;
   }
-  const bool want_dgb = grad_gb != nullptr && !copy && num_edges > 0;
+  const bool want_dgb = grad_gb != nullptr && !copy && num_edges > 0 && agg_scale != 0.f;
   const bool want_dx = grad_x != nullptr;
   if (!want_dgb && !want_dx) return hipSuccess;
   if (num_graphs == 0 || num_nodes == 0 || max_nodes == 0 || C == 0 || P == 0) return hipSuccess;
@@ -96,6 +109,9 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
   a.dxb = want_dx ? grad_x_base : nullptr;
   a.dxbs = base_node_stride;
   a.kdeg = kdeg;
+  a.agg_scale = agg_scale;
+  a.self_scale = self_scale;
+  a.epi = (agg_scale != 1.f || self_scale != 0.f) ? 1 : 0;
   return dispatch_bwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, st);
 }
 

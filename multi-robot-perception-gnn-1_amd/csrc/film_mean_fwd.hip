@@ -1,13 +1,32 @@
 // film_mean_fwd.hip — forward launchers and C ABI (mrp_film_mean_fwd, mrp_film_mean_cat_fwd).
 // Kernels and design notes: film_mean_kernels.hpp.
+#include <cstring>
+
 #include "film_mean_kernels.hpp"
 
 using namespace mrp_host;
 
 namespace {
 
+template <int NT, int KMAX>
+hipError_t launch_fwd_regular(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  const size_t lds = lds_fwd_regular<NT, KMAX>(g.cpb);
+  if (g.vec == 4)
+    MRP_LAUNCH((mrp::film_fwd_regular<NT, KMAX, 4>), lds);
+  else if (g.vec == 1)
+    MRP_LAUNCH((mrp::film_fwd_regular<NT, KMAX, 1>), lds);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 template <int NT, bool COMPLETE>
 hipError_t launch_fwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  if constexpr (!COMPLETE) {
+    // per-edge-slot weights for uniform in-degree (k-NN frames)
+    if (a.kdeg >= 1 && a.kdeg <= 4) return launch_fwd_regular<NT, 4>(a, g, st);
+    if (a.kdeg >= 5 && a.kdeg <= 8) return launch_fwd_regular<NT, 8>(a, g, st);
+  }
   const size_t lds = lds_fwd<NT>(g.cpb);
   if (g.vec == 4)
     MRP_LAUNCH((mrp::film_fwd<NT, 4, COMPLETE>), lds);
@@ -23,11 +42,24 @@ hipError_t launch_fwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
 hipError_t dispatch_fwd(int nt, bool complete, const AggArgs& a, const Geometry& g, hipStream_t st) {
   MRP_DISPATCH_NT(nt, complete, launch_fwd_nt, a, g, st)
 }
+
+// REGULAR graphs: split the plane over workgroups like COMPLETE graphs (their prologue is two
+// rounds of loads, not a CSR walk).  An experiment knob (mrp_tuning_set).
+bool fwd_regular_split = true;
 }  // namespace
 
 extern "C" {
 
-int mrp_abi_version(void) { return 9; }
+int mrp_abi_version(void) { return 10; }
+
+int mrp_tuning_set(const char* name, int32_t value) {
+  if (name == nullptr) return hipErrorInvalidValue;
+  if (std::strcmp(name, "fwd_regular_split") == 0) {
+    fwd_regular_split = value != 0;
+    return hipSuccess;
+  }
+  return hipErrorInvalidValue;
+}
 
 const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
 
@@ -38,7 +70,11 @@ namespace {
 int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr, const int32_t* src,
                   const int32_t* eid, const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes,
                   int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode_flags,
-                  float* out, int64_t out_node_stride, float* xcopy, int64_t xcopy_node_stride, void* stream) {
+                  float* out, int64_t out_node_stride, const mrp_agg_epilogue* ep, void* stream) {
+  float* xcopy = ep != nullptr ? ep->xcopy : nullptr;
+  const int64_t xcopy_node_stride = ep != nullptr ? ep->xcopy_node_stride : 0;
+  const float* x0 = ep != nullptr ? ep->x0 : nullptr;
+  const int64_t x0_node_stride = ep != nullptr ? ep->x0_node_stride : 0;
   const int32_t logits = (mode_flags & MRP_AGG_GB_LOGITS) ? 1 : 0;
   const int32_t mode = mode_flags & ~MRP_AGG_GB_LOGITS;
   if (!common_args_ok(indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind, num_nodes, num_edges, C, P,
@@ -50,9 +86,13 @@ int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const 
     return hipErrorInvalidValue;
   if (mode != MRP_AGG_COPY_MEAN && num_edges > 0 && gb == nullptr) return hipErrorInvalidValue;
   if (xcopy != nullptr && xcopy_node_stride < plane) return hipErrorInvalidValue;
+  if (x0 != nullptr && x0_node_stride < plane) return hipErrorInvalidValue;
   bool vec4 =
       (P % 4 == 0) && (x_node_stride % 4 == 0) && (out_node_stride % 4 == 0) && aligned16(x) && aligned16(out);
   if (xcopy != nullptr) vec4 = vec4 && (xcopy_node_stride % 4 == 0) && aligned16(xcopy);
+  if (x0 != nullptr) vec4 = vec4 && (x0_node_stride % 4 == 0) && aligned16(x0);
+  const int32_t kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
+  const bool regular = kdeg >= 1 && kdeg <= 8;
   // 16-byte slices beat 8-byte ones at every measured size (tools/kernel_lab.hip product sweep)
   Geometry g = make_geometry(C, P, vec4 ? 4 : 1, 16, 64, mrp::kMaxChanPerBlock);
   // COMPLETE graphs: one slice per lane, the plane split over ceil(PV / lpc) workgroups (their
@@ -60,7 +100,9 @@ int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const 
   // graphs keep whole planes: their prologue walks the CSR (dependent loads) and a split repeats it
   // per segment (k-NN(4) N=16 C=1024 16x16: 304 us split vs 225 us whole)
   const int32_t pv = P / g.vec;
-  const int32_t psplit = graph_kind == MRP_GRAPH_COMPLETE ? (pv + g.lpc - 1) / g.lpc : 1;
+  const int32_t psplit = (graph_kind == MRP_GRAPH_COMPLETE || (regular && fwd_regular_split))
+                             ? (pv + g.lpc - 1) / g.lpc
+                             : 1;
   g.grid = (int64_t)num_graphs * g.ncb * psplit;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
   AggArgs a = {};
@@ -84,7 +126,16 @@ int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const 
   a.xc = xcopy;
   a.xcs = xcopy_node_stride;
   a.psplit = psplit;
-  a.kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
+  a.kdeg = kdeg;
+  a.agg_scale = 1.f;
+  if (ep != nullptr) {
+    a.agg_scale = ep->agg_scale;
+    a.self_scale = ep->self_scale;
+    a.x0 = x0;
+    a.x0s = x0_node_stride;
+    a.x0_scale = ep->x0_scale;
+    a.epi = (ep->agg_scale != 1.f || ep->self_scale != 0.f || x0 != nullptr) ? 1 : 0;
+  }
   return dispatch_fwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, static_cast<hipStream_t>(stream));
 }
 
@@ -97,7 +148,16 @@ int mrp_film_mean_fwd(const float* x, int64_t x_node_stride, const float* gb, co
                       int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C,
                       int32_t P, int32_t mode_flags, float* out, int64_t out_node_stride, void* stream) {
   return film_fwd_impl(x, x_node_stride, gb, indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind,
-                       num_nodes, num_edges, C, P, mode_flags, out, out_node_stride, nullptr, 0, stream);
+                       num_nodes, num_edges, C, P, mode_flags, out, out_node_stride, nullptr, stream);
+}
+
+int mrp_film_mean_fwd_ex(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr,
+                         const int32_t* src, const int32_t* eid, const int32_t* graph_off, int32_t num_graphs,
+                         int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C,
+                         int32_t P, int32_t mode_flags, float* out, int64_t out_node_stride,
+                         const mrp_agg_epilogue* epilogue, void* stream) {
+  return film_fwd_impl(x, x_node_stride, gb, indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind,
+                       num_nodes, num_edges, C, P, mode_flags, out, out_node_stride, epilogue, stream);
 }
 
 int mrp_film_mean_cat_fwd(const float* x, int64_t x_node_stride, const float* gb, const int32_t* indptr,
@@ -105,9 +165,9 @@ int mrp_film_mean_cat_fwd(const float* x, int64_t x_node_stride, const float* gb
                           int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges, int32_t C,
                           int32_t P, int32_t mode_flags, float* cat, int64_t cat_node_stride, void* stream) {
   if (cat == nullptr || cat_node_stride < 2 * (int64_t)C * P) return hipErrorInvalidValue;
+  mrp_agg_epilogue ep = {1.f, 0.f, nullptr, 0, 0.f, cat, cat_node_stride};
   return film_fwd_impl(x, x_node_stride, gb, indptr, src, eid, graph_off, num_graphs, max_nodes, graph_kind,
-                       num_nodes, num_edges, C, P, mode_flags, cat + (int64_t)C * P, cat_node_stride, cat,
-                       cat_node_stride, stream);
+                       num_nodes, num_edges, C, P, mode_flags, cat + (int64_t)C * P, cat_node_stride, &ep, stream);
 }
 
 }  // extern "C"

@@ -71,7 +71,43 @@ struct AggArgs {
   float* xc;       // forward: optional copy of x (the first half of a concatenation buffer)
   int64_t xcs;     // its node stride
   int32_t psplit;  // forward: plane segments per (graph, channel block) (0 or 1: whole plane)
+  // epilogue (mrp_agg_epilogue): forward out = agg_scale*a + self_scale*x[v] + x0_scale*x0[v];
+  // backward: grad_out reaches the aggregate scaled by agg_scale (folded into the reduce scale s_v),
+  // and self_scale*grad_out[u] is added to grad_x[u].  epi = 0: plain (agg_scale 1, the rest 0).
+  int32_t epi;
+  float agg_scale, self_scale, x0_scale;
+  const float* x0;
+  int64_t x0s;
 };
+
+// Forward epilogue of destination `node`, channel c, slice at `off` (see AggArgs::epi).
+template <int VEC>
+__device__ __forceinline__ void apply_epilogue(const AggArgs& a, float* acc, const float* xself, int node, int c,
+                                               int64_t off) {
+  if (a.agg_scale != 1.f) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = __fmul_rn(a.agg_scale, acc[k]);
+  }
+  if (a.self_scale != 0.f) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(a.self_scale, xself[k]));
+  }
+  if (a.x0 != nullptr) {
+    const float* p = a.x0 + (int64_t)node * a.x0s + (int64_t)c * a.P + off;
+    float z[VEC];
+    if constexpr (VEC == 4) {
+      const f4 t = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+      z[0] = t.x; z[1] = t.y; z[2] = t.z; z[3] = t.w;
+    } else if constexpr (VEC == 2) {
+      const f2 t = __builtin_nontemporal_load(reinterpret_cast<const f2*>(p));
+      z[0] = t.x; z[1] = t.y;
+    } else {
+      z[0] = __builtin_nontemporal_load(p);
+    }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(a.x0_scale, z[k]));
+  }
+}
 
 __device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
 
@@ -135,6 +171,16 @@ __device__ __forceinline__ void store_frag(float* p, const Frag<VEC>& f) {
   }
 }
 
+// Wave-uniform base + 32-bit lane byte offset: lets the compiler use the SGPR-base form of
+// global_load/store (saddr + 32-bit vaddr) instead of a 64-bit VGPR address per access — with N
+// source and N destination planes per slice those addresses are most of a kernel's VGPRs.
+__device__ __forceinline__ const float* at_bytes(const float* base, uint32_t off) {
+  return reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + off);
+}
+__device__ __forceinline__ float* at_bytes(float* base, uint32_t off) {
+  return reinterpret_cast<float*>(reinterpret_cast<char*>(base) + off);
+}
+
 template <int NT>
 struct Tile {
   static constexpr int NTP = (NT + 3) & ~3;  // padded row -> 16-byte aligned LDS rows
@@ -195,6 +241,7 @@ __device__ __forceinline__ void build_tiles_csr(const AggArgs& a, int node0, int
       const int deg = end - beg;
       float s = 1.f;
       if (BWD && a.mode != MRP_AGG_FILM_SUM && deg > 0) s = 1.f / (float)deg;
+      if (BWD) s *= a.agg_scale;  // epilogue: grad_out reaches the aggregate scaled
       unsigned mask = 0u;
       // In-edges in chunks of KC, every load of a chunk issued before any is consumed (indices
       // clamped instead of branched around, so the loads stay independent); accumulation stays
@@ -286,7 +333,8 @@ __device__ __forceinline__ void complete_store(const AggArgs& a, int base, const
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
   const int tot = a.cpb * S;
-  const float s = (BWD && a.mode != MRP_AGG_FILM_SUM && NT > 1) ? 1.f / (float)(NT - 1) : 1.f;
+  const float s = ((BWD && a.mode != MRP_AGG_FILM_SUM && NT > 1) ? 1.f / (float)(NT - 1) : 1.f) *
+                  (BWD ? a.agg_scale : 1.f);
 #pragma unroll
   for (int r = 0; r < CompleteSlots<NT>::kPer; ++r) {
     const int t = base + threadIdx.x + r * blockDim.x;
@@ -352,8 +400,10 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   const int li = threadIdx.x - grp * a.lpc;
   const int c = c0 + grp;
   const bool active = grp < a.cpb && c < a.C;
-  const float* xb = a.x + (int64_t)node0 * a.xs + (int64_t)c * a.P;
-  float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
+  // uniform per-graph/channel-block bases, per-lane 32-bit byte offsets (see at_bytes)
+  const float* xb = a.x + (int64_t)node0 * a.xs + (int64_t)c0 * a.P;
+  float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c0 * a.P;
+  const uint32_t lane_plane = (uint32_t)grp * (uint32_t)a.P * 4u;
 
   // prologue part 1 (COMPLETE): gamma/beta into registers
   float2 reg[CompleteSlots<NT>::kPer];
@@ -361,14 +411,21 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   if (COMPLETE) complete_fetch<NT>(a, ebase, c0, 0, reg);
   // first slice of the sweep, issued before the weight tiles are needed
   int j = jbeg + li;
-  Frag<VEC> xv[NT];
-  if (active && j < jend) {
+  // element k of every source's slice in one NT-wide vector value: when the compiler keeps a
+  // neighbour loop rolled (CSR, NT > 8) the source index is a dynamic extract from registers,
+  // not an indexed private array (which spilled 272 B/lane to scratch at NT = 16)
+  typedef float vnt __attribute__((ext_vector_type(NT <= 4 ? 4 : (NT <= 8 ? 8 : 16))));
+  vnt xv[VEC];
+  auto load_slice = [&](int jj) {
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
       const int uu = u < n ? u : n - 1;  // clamp (ragged batch); never used for output
-      xv[u] = load_frag<VEC, true>(xb + (int64_t)uu * a.xs + (int64_t)j * VEC);
+      const Frag<VEC> f = load_frag<VEC, true>(at_bytes(xb + (int64_t)uu * a.xs, lane_plane + (uint32_t)jj * VEC * 4u));
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) xv[k][u] = f.v[k];
     }
-  }
+  };
+  if (active && j < jend) load_slice(j);
   // prologue part 2: tiles into LDS
   if (COMPLETE) {
     complete_store<NT, false>(a, 0, reg, Ga, Gb);
@@ -394,6 +451,7 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
 
   while (j < jend) {
     const int64_t off = (int64_t)j * VEC;
+    const uint32_t lane_off = lane_plane + (uint32_t)j * VEC * 4u;
     // Re-read the tiles from LDS every slice: laundering the tile offset stops the compiler from
     // hoisting all N*N weights into registers (which would cost occupancy or spill).
     int tile = grp * SZ;
@@ -426,7 +484,7 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
           const float gbv = wb[q];
 #pragma unroll
           for (int k = 0; k < VEC; ++k) {
-            const float m = film ? __fadd_rn(__fmul_rn(ga, xv[u].v[k]), gbv) : __fmul_rn(ga, xv[u].v[k]);
+            const float m = film ? __fadd_rn(__fmul_rn(ga, xv[k][u]), gbv) : __fmul_rn(ga, xv[k][u]);
             acc.v[k] = __fadd_rn(acc.v[k], m);
           }
         }
@@ -440,26 +498,188 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc.v[k] = acc.v[k] / d;
       }
-      store_frag<VEC, true>(ob + (int64_t)v * a.os + off, acc);
+      if (a.epi) {
+        float xself[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) xself[k] = xv[k][v];
+        apply_epilogue<VEC>(a, acc.v, xself, node0 + v, c, off);
+      }
+      store_frag<VEC, true>(at_bytes(ob + (int64_t)v * a.os, lane_off), acc);
     }
     if (a.xc != nullptr) {
       // cat((x, aggregate), 1): the slices of x are in registers already; writing them here saves
       // the separate copy's read of x
-      float* xcb = a.xc + (int64_t)node0 * a.xcs + (int64_t)c * a.P + off;
+      float* xcb = a.xc + (int64_t)node0 * a.xcs + (int64_t)c0 * a.P;
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         if (u >= n) break;
-        store_frag<VEC, true>(xcb + (int64_t)u * a.xcs, xv[u]);
+        Frag<VEC> f;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) f.v[k] = xv[k][u];
+        store_frag<VEC, true>(at_bytes(xcb + (int64_t)u * a.xcs, lane_off), f);
       }
     }
     j += a.lpc;
-    if (j < jend) {
+    if (j < jend) load_slice(j);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Forward for REGULAR graphs (every node has exactly K = a.kdeg <= KMAX in-edges: k-NN frames).
+// Per-edge-slot weights instead of the dense N x N tiles: slot (v, j) is v's j-th in-edge in CSR
+// (= edge id = DGL mailbox) order, its (gamma, beta) for the workgroup's channels and its local
+// source u(v, j) sit in LDS.  The sweep makes exactly K multiply-adds per destination and element,
+// with no per-neighbour branches: u(v, j) is the same for the whole workgroup, so x_u is a
+// wave-uniform dynamic index into the slice registers (lowered to M0-relative moves, no scratch).
+// Summation order = slot order, as the mailbox mean: acc = fl(acc + fl(fl(gamma x_u) + beta)),
+// out = fl(acc / K).  Like film_fwd with COMPLETE graphs, the plane may be split over psplit
+// workgroups (the prologue is two rounds of loads: CSR slots, then gamma/beta).
+// ---------------------------------------------------------------------------
+template <int NT, int KMAX, int VEC>
+__global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
+  constexpr int NS = NT * KMAX;
+  constexpr int WPD = KMAX / 4;  // 32-bit words of packed 8-bit slot sources per destination
+  static_assert(KMAX % 4 == 0, "slots are packed four to a word");
+  extern __shared__ float4 smem_f4[];
+  float2* Wl = reinterpret_cast<float2*>(smem_f4);                  // [cpb][NS] (gamma, beta) per slot
+  unsigned* slot_u = reinterpret_cast<unsigned*>(Wl + a.cpb * NS);  // [NT * WPD] packed local sources
+  int* slot_e = reinterpret_cast<int*>(slot_u + NT * WPD);          // [NS] edge id of the slot (-1: none)
+
+  const int ps = a.psplit > 1 ? a.psplit : 1;
+  const int item = blockIdx.x / ps;
+  const int seg = blockIdx.x - item * ps;
+  const int b = item / a.ncb;
+  const int cb = item - b * a.ncb;
+  const int seglen = (a.PV + ps - 1) / ps;
+  const int jbeg = seg * seglen;
+  const int jend = min(a.PV, jbeg + seglen);
+  const int node0 = a.goff[b];
+  const int n = min(a.goff[b + 1] - node0, NT);
+  if (n <= 0) return;
+  const int c0 = cb * a.cpb;
+  const int K = a.kdeg;
+
+  const int grp = threadIdx.x / a.lpc;
+  const int li = threadIdx.x - grp * a.lpc;
+  const int c = c0 + grp;
+  const bool active = grp < a.cpb && c < a.C;
+  // uniform per-graph/channel-block bases, per-lane 32-bit byte offsets (see at_bytes)
+  const float* xb = a.x + (int64_t)node0 * a.xs + (int64_t)c0 * a.P;
+  float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c0 * a.P;
+  const uint32_t lane_plane = (uint32_t)grp * (uint32_t)a.P * 4u;
+
+  // First slice's loads, issued before the prologue's two dependent rounds.  Element k of every
+  // source's slice lives in one NT-wide vector value, so the wave-uniform source index is a dynamic
+  // extract from a register tuple (s_set_gpr_idx / v_movrels), not an indexed private array.
+  typedef float vnt __attribute__((ext_vector_type(NT <= 8 ? 8 : 16)));
+  int j = jbeg + li;
+  vnt xs[VEC];
+  auto load_slice = [&](int jj) {
 #pragma unroll
-      for (int u = 0; u < NT; ++u) {
-        const int uu = u < n ? u : n - 1;
-        xv[u] = load_frag<VEC, true>(xb + (int64_t)uu * a.xs + (int64_t)j * VEC);
+    for (int u = 0; u < NT; ++u) {
+      const int uu = u < n ? u : n - 1;
+      const Frag<VEC> f = load_frag<VEC, true>(at_bytes(xb + (int64_t)uu * a.xs, lane_plane + (uint32_t)jj * VEC * 4u));
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) xs[k][u] = f.v[k];
+    }
+  };
+  if (active && j < jend) load_slice(j);
+
+  // prologue 1: the graph's slots (channel-independent)
+  for (int t = threadIdx.x; t < NT * WPD; t += blockDim.x) {
+    const int v = t / WPD, q = t - v * WPD;
+    unsigned word = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int jj = q * 4 + i;
+      int u = 0, e = -1;
+      if (v < n && jj < K) {
+        const int k = (node0 + v) * K + jj;  // REGULAR: v's CSR row is [K*v, K*(v+1))
+        u = a.src[k] - node0;
+        e = a.eid[k];
+        if ((unsigned)u >= (unsigned)n) { u = 0; e = -1; }  // leaves the graph: rejected on the host
+      }
+      word |= (unsigned)u << (8 * i);
+      slot_e[v * KMAX + jj] = e;
+    }
+    slot_u[t] = word;
+  }
+  __syncthreads();
+  // prologue 2: (gamma, beta) of every (channel, slot); an empty slot multiplies by 0 and adds 0
+  for (int t = threadIdx.x; t < a.cpb * NS; t += blockDim.x) {
+    int cl, slot;  // channel fastest: neighbouring lanes read neighbouring gamma/beta pairs
+    split_channel(a, t, cl, slot);
+    const int cc = c0 + cl;
+    const int e = slot_e[slot];
+    float2 w = make_float2(0.f, 0.f);
+    if (e >= 0 && cc < a.C) {
+      if (a.mode == MRP_AGG_COPY_MEAN) {
+        w = make_float2(1.f, 0.f);  // gamma 1, beta 0: fl(fl(1*x) + 0) = x
+      } else {
+        w = *reinterpret_cast<const float2*>(a.gb + ((int64_t)e * a.C + cc) * 2);
+        if (a.logits) w = make_float2(sigmoidf(w.x), sigmoidf(w.y));
       }
     }
+    Wl[cl * NS + slot] = w;
+  }
+  __syncthreads();
+  if (!active) return;
+
+  const bool mean = a.mode != MRP_AGG_FILM_SUM;
+  const float d = (float)K;
+  while (j < jend) {
+    const int64_t off = (int64_t)j * VEC;
+    const uint32_t lane_off = lane_plane + (uint32_t)j * VEC * 4u;
+    // every destination row is computed (full unroll); rows past the graph's nodes are not stored
+#pragma unroll
+    for (int v = 0; v < NT; ++v) {
+      int wbase = grp * NS;  // laundered: weights stay in LDS (broadcast reads), not hoisted
+      asm volatile("" : "+v"(wbase));
+      const float2* Wc = Wl + wbase;
+      unsigned uw[WPD];
+#pragma unroll
+      for (int q = 0; q < WPD; ++q) uw[q] = __builtin_amdgcn_readfirstlane(slot_u[v * WPD + q]);
+      float acc[VEC];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < KMAX; ++jj) {
+        if (jj >= K) break;  // wave-uniform
+        const int u = (uw[jj >> 2] >> (8 * (jj & 3))) & 0xffu;
+        const float2 w = Wc[v * KMAX + jj];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], __fadd_rn(__fmul_rn(w.x, xs[k][u]), w.y));
+      }
+      if (mean) {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[k] = acc[k] / d;
+      }
+      if (a.epi) {
+        float xself[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) xself[k] = xs[k][v];
+        apply_epilogue<VEC>(a, acc, xself, node0 + v, c, off);
+      }
+      if (v < n) {
+        Frag<VEC> o;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) o.v[k] = acc[k];
+        store_frag<VEC, true>(at_bytes(ob + (int64_t)v * a.os, lane_off), o);
+      }
+    }
+    if (a.xc != nullptr) {
+      float* xcb = a.xc + (int64_t)node0 * a.xcs + (int64_t)c0 * a.P;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        if (u >= n) break;
+        Frag<VEC> f;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) f.v[k] = xs[k][u];
+        store_frag<VEC, true>(at_bytes(xcb + (int64_t)u * a.xcs, lane_off), f);
+      }
+    }
+    j += a.lpc;
+    if (j < jend) load_slice(j);
   }
 }
 
@@ -521,6 +741,10 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
       } else {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
+      }
+      if (a.self_scale != 0.f) {  // residual epilogue: d out / d x[u] includes self_scale
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(a.self_scale, gv[u].v[k], acc.v[k]);
       }
 #pragma unroll
       for (int v4 = 0; v4 < NTP; v4 += 4) {
@@ -680,6 +904,10 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
 #pragma unroll
               for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
             }
+            if (a.self_scale != 0.f) {  // residual epilogue (one pass: gv[u] is node u's grad_out)
+#pragma unroll
+              for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(a.self_scale, gv[u].v[k], acc.v[k]);
+            }
 #pragma unroll
             for (int v4 = 0; v4 < NTP; v4 += 4) {
               const f4 w = *reinterpret_cast<const f4*>(W + u * NTP + v4);
@@ -745,7 +973,7 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   __syncthreads();
   if (COMPLETE) {
     // Per-edge outputs: thread -> (channel fastest, slot (v, u)); arithmetic edge ids.
-    const float s = (a.mode != MRP_AGG_FILM_SUM && NT > 1) ? 1.f / (float)(NT - 1) : 1.f;
+    const float s = ((a.mode != MRP_AGG_FILM_SUM && NT > 1) ? 1.f / (float)(NT - 1) : 1.f) * a.agg_scale;
     const int64_t ebase = (int64_t)b * NT * (NT - 1);
     for (int t = threadIdx.x; t < a.cpb * NT * NT; t += blockDim.x) {
       int cl, slot;
@@ -895,6 +1123,10 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
 #pragma unroll
             for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
           }
+          if (a.self_scale != 0.f) {  // residual epilogue
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(a.self_scale, gv[u][k], acc.v[k]);
+          }
 #pragma unroll
           for (int v4 = 0; v4 < NTP; v4 += 4) {
             const f4 w = *reinterpret_cast<const f4*>(W + u * NTP + v4);
@@ -1003,6 +1235,11 @@ inline Geometry make_geometry(int C, int P, int vec, int lo, int hi, int max_cpb
 template <int NT>
 size_t lds_fwd(int cpb) {
   return (size_t)(2 * cpb * mrp::Tile<NT>::SZ + 2 * mrp::Tile<NT>::NTP) * sizeof(float);
+}
+template <int NT, int KMAX>
+size_t lds_fwd_regular(int cpb) {
+  return (size_t)cpb * NT * KMAX * sizeof(float2) + (size_t)NT * (KMAX / 4) * sizeof(unsigned) +
+         (size_t)NT * KMAX * sizeof(int);
 }
 template <int NT>
 size_t lds_dx(int cpb) {

@@ -9,6 +9,9 @@ Mirrors ``dgl/model/models.py``:
 * :class:`GCNBlock`      — the GCN stacking of ``multi_view_dgl_model.forward`` (``models.py:180-189``):
   ``gcn1 -> cat -> [conv1] -> [gcn2 -> cat -> conv2]``, keys ``gcn1.*``, ``conv1.*``, ``gcn2.*``, ``conv2.*``;
   the 1x1 convs run as batched GEMMs (``compress.py``).
+* :class:`GCNStack`      — the same for k layers (``opt.gcn_layers``; BASELINE configs[4] runs 3) and
+  the residual (``dgl_models.py:36-37``) / initial-feature-mix combinations, each fused into the
+  aggregation kernel's epilogue.
 * :class:`multi_view_dgl_model` — ``models.py:157-205`` with the CNN encoder/decoder supplied by the
   caller (they are torchvision/dense-conv code outside the hot path), so a reference
   ``encoder``/``decoder`` instance can be plugged in unchanged.
@@ -30,7 +33,7 @@ import warnings
 import torch
 import torch.nn as nn
 
-from .aggregate import film_mean, film_mean_cat
+from .aggregate import film_mean, film_mean_cat, film_mean_mix, film_mean_residual
 from .compress import compress_1x1
 from .encoder import edge_logits
 
@@ -126,27 +129,108 @@ class GCN(nn.Module):
         return film_mean_cat(x, z, g.csr(x.device), mode, logits=True)
 
 
-class GCNBlock(nn.Module):
-    """GCN stacking of ``multi_view_dgl_model`` (``dgl/model/models.py:162-171,180-189``)."""
+    def forward_residual(self, g, feats: torch.Tensor = None) -> torch.Tensor:
+        """``feats + self(g, feats)`` in one kernel pass: the residual combination ``h = g_h + h``
+        of ``dgl/model/dgl_models.py:36-37`` (the FiLM-mean 'add' variant)."""
+        x = g.ndata["image"] if feats is None else feats
+        if self._return_mode() == "input" or not x.is_cuda:
+            return x + self(g, x)
+        mode = _opt(self.opt, "gcn_mode", "film_mean")
+        if mode == "copy_mean":
+            return film_mean_residual(x, None, g.csr(x.device), mode)
+        z = self.edge_encoder.logits(g.edata["pose"])
+        return film_mean_residual(x, z, g.csr(x.device), mode, logits=True)
+
+    def forward_mix(self, g, feats: torch.Tensor, x0: torch.Tensor, alpha: float) -> torch.Tensor:
+        """``(1 - alpha) * self(g, feats) + alpha * x0`` in one kernel pass: a GCN2-style
+        initial-feature mix (BASELINE configs[3]'s "GCN2Conv"; not in the reference)."""
+        x = feats
+        if self._return_mode() == "input" or not x.is_cuda:
+            return (1.0 - alpha) * self(g, x) + alpha * x0
+        mode = _opt(self.opt, "gcn_mode", "film_mean")
+        if mode == "copy_mean":
+            return film_mean_mix(x, None, g.csr(x.device), x0, alpha, mode)
+        z = self.edge_encoder.logits(g.edata["pose"])
+        return film_mean_mix(x, z, g.csr(x.device), x0, alpha, mode, logits=True)
+
+
+#: layer compositions of a GCN stack (``GCNStack``, ``multi_view_dgl_model``)
+COMBINES = ("cat_compress", "cat", "residual", "initial_mix")
+
+
+def stack_layout(opt):
+    """(number of GCN layers, combine, 1x1 compress convs?) from the reference flags
+    (``compress_gcn``, ``multi_gcn``, ``models.py:162-171``) or their generalisation
+    ``opt.gcn_layers`` / ``opt.gcn_combine``:
+
+    * ``'cat_compress'`` — ``h = conv_i(cat(h, gcn_i(h)))`` per layer (``models.py:180-189``;
+      ``multi_gcn`` is two such layers; k layers extend the ``gcn<i>``/``conv<i>`` naming);
+    * ``'cat'`` — one layer, ``h = cat(h, gcn1(h))`` (2C channels; ``compress_gcn`` off);
+    * ``'residual'`` — ``h = h + gcn_i(h)`` (``dgl_models.py:36-37``), no convs;
+    * ``'initial_mix'`` — ``h = (1 - alpha) gcn_i(h) + alpha h0`` (``opt.gcn2_alpha``, default 0.1;
+      GCN2-style extension, not in the reference), no convs."""
+    layers = int(_opt(opt, "gcn_layers", 0) or (2 if _opt(opt, "multi_gcn", False) else 1))
+    combine = _opt(opt, "gcn_combine", None)
+    if combine is None:
+        combine = "cat_compress" if _opt(opt, "compress_gcn", False) else "cat"
+    if combine not in COMBINES:
+        raise ValueError(f"gcn_combine must be one of {COMBINES}, got {combine!r}")
+    if layers < 1:
+        raise ValueError("gcn_layers must be >= 1")
+    if combine == "cat" and layers > 1:
+        raise AssertionError("stacked GCN layers need compress_gcn (models.py:169)")
+    return layers, combine, combine == "cat_compress"
+
+
+def _build_stack(module: nn.Module, opt) -> None:
+    layers, combine, convs = stack_layout(opt)
+    module.gcn_layers, module.gcn_combine = layers, combine
+    for i in range(1, layers + 1):
+        setattr(module, f"gcn{i}", GCN(opt))
+        if convs:
+            setattr(module, f"conv{i}", nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1))
+
+
+def _run_stack(module: nn.Module, g, h: torch.Tensor) -> torch.Tensor:
+    """The layer loop of ``multi_view_dgl_model.forward`` (``models.py:180-189``), k layers."""
+    h0 = h
+    alpha = float(_opt(module.opt, "gcn2_alpha", 0.1))
+    for i in range(1, module.gcn_layers + 1):
+        gcn = getattr(module, f"gcn{i}")
+        if module.gcn_combine in ("cat_compress", "cat"):
+            h = gcn.forward_cat(g, h)  # cat((h, gcn_i(h)), 1), one kernel pass
+            if module.gcn_combine == "cat_compress":
+                h = compress_1x1(getattr(module, f"conv{i}"), h)
+        elif module.gcn_combine == "residual":
+            h = gcn.forward_residual(g, h)
+        else:
+            h = gcn.forward_mix(g, h, h0, alpha)
+    return h
+
+
+class GCNStack(nn.Module):
+    """k stacked GCN layers (``dgl/model/models.py:162-171,180-189`` generalised; see
+    :func:`stack_layout`).  ``state_dict`` keys ``gcn1.*``, ``conv1.*``, ..., ``gcn<k>.*``,
+    ``conv<k>.*`` — the reference's naming for k = 1, 2."""
 
     def __init__(self, opt):
         super().__init__()
         self.opt = opt
-        self.gcn1 = GCN(opt)
-        if opt.compress_gcn:
-            self.conv1 = nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1)
-        if opt.multi_gcn:
-            assert opt.compress_gcn  # models.py:169
-            self.gcn2 = GCN(opt)
-            self.conv2 = nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1)
+        _build_stack(self, opt)
 
     def forward(self, g, h: torch.Tensor) -> torch.Tensor:
-        h = self.gcn1.forward_cat(g, h)  # cat((h, gcn1(h)), 1)
-        if self.opt.compress_gcn:
-            h = compress_1x1(self.conv1, h)
-        if self.opt.multi_gcn:
-            h = compress_1x1(self.conv2, self.gcn2.forward_cat(g, h))
-        return h
+        return _run_stack(self, g, h)
+
+
+class GCNBlock(GCNStack):
+    """GCN stacking of ``multi_view_dgl_model`` (``dgl/model/models.py:162-171,180-189``): gcn1 ->
+    cat -> [conv1] -> [gcn2 -> cat -> conv2] from the reference's ``compress_gcn``/``multi_gcn``
+    flags (a :class:`GCNStack` of one or two layers)."""
+
+    def __init__(self, opt):
+        if opt.multi_gcn:
+            assert opt.compress_gcn  # models.py:169
+        super().__init__(opt)
 
 
 class multi_view_dgl_model(nn.Module):  # noqa: N801  (reference class name)
@@ -163,15 +247,16 @@ class multi_view_dgl_model(nn.Module):  # noqa: N801  (reference class name)
         self.opt = opt
         if encoder is not None:
             self.encoder = encoder
-        self.gcn1 = GCN(opt)
-        if opt.compress_gcn:
-            self.conv1 = nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1)
+        if _opt(opt, "multi_gcn", False):
+            assert opt.compress_gcn  # models.py:169
+        _build_stack(self, opt)  # gcn1 [conv1] [gcn2 conv2] ... (models.py:162-171)
         if decoder is not None:
             self.decoder = decoder
-        if opt.multi_gcn:
-            assert opt.compress_gcn
-            self.gcn2 = GCN(opt)
-            self.conv2 = nn.Conv2d(opt.feature_dim * 2, opt.feature_dim, kernel_size=1)
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        if "gcn_layers" not in self.__dict__:  # pickled by the reference: its flags give the layout
+            self.gcn_layers, self.gcn_combine, _ = stack_layout(self.opt)
 
     def features(self, g):
         """Encoder output per node, (B*N, C, h, w), and the encoder's feature list
@@ -201,10 +286,5 @@ class multi_view_dgl_model(nn.Module):  # noqa: N801  (reference class name)
         with g.local_scope():
             h, h_list = self.features(g)
             g.ndata["image"] = h
-            h = self.gcn1.forward_cat(g)  # cat((h, gcn1(g)), 1), models.py:181-182
-            if self.opt.compress_gcn:
-                h = compress_1x1(self.conv1, h)
-            if self.opt.multi_gcn:
-                g.ndata["image"] = h
-                h = compress_1x1(self.conv2, self.gcn2.forward_cat(g))  # models.py:186-189
+            h = _run_stack(self, g, h)  # gcn1 -> cat -> conv1 [-> gcn2 -> cat -> conv2], models.py:180-189
             return self.decode(h, h_list)

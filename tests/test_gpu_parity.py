@@ -366,8 +366,11 @@ def regular_graph(n, k, rng, multi=False):
 @pytest.mark.parametrize("hw", [(8, 8), (3, 5)])
 @pytest.mark.parametrize("multi", [False, True])
 def test_regular_backward_equals_csr_path(cuda_device, n, k, hw, multi):
-    """The per-edge-slot backward of regular graphs (film_bwd_regular) against the oracle and the
-    general CSR kernels, for mixed graph sizes, multi-edges/self-loops and both slice widths."""
+    """The per-edge-slot kernels of regular graphs (film_fwd_regular, film_bwd_regular) against the
+    oracle and the general CSR kernels, for mixed graph sizes, unsorted in-edges, multi-edges /
+    self-loops and both slice widths.  The per-slot forward sums each mailbox in edge-id order, as
+    DGL does, so it is bit-identical to the oracle wherever the oracle's sum is sequential; the dense
+    CSR kernel sums by ascending source (and merges multi-edges), so it agrees to rounding."""
     rng = np.random.RandomState(n * 31 + k)
     small = max(k, n - 3)
     g = m.batch([regular_graph(n, k, rng, multi), regular_graph(small, k, rng, multi), regular_graph(n, k, rng, multi)])
@@ -387,7 +390,14 @@ def test_regular_backward_equals_csr_path(cuda_device, n, k, hw, multi):
         out = m.film_mean_cat(xd, zd, csr, logits=True)
         out.backward(torch.cat((G, G), 1).to(cuda_device))
         res.append((out.detach().cpu(), xd.grad.cpu(), zd.grad.cpu()))
-    assert torch.equal(res[0][0], res[1][0])
+    out_ref = oracle.film_aggregate(x, torch.sigmoid(z), src, dst)
+    assert torch.equal(res[0][0][:, :12], x) and torch.equal(res[1][0][:, :12], x)
+    if 12 * hw[0] * hw[1] % 64 == 0:  # the oracle's (CPU torch) mailbox mean is a sequential sum
+        # gamma/beta given post-sigmoid (the device sigmoid's expf rounds differently from torch's)
+        exact = m.film_mean(x.to(cuda_device), torch.sigmoid(z).to(cuda_device), fast).cpu()
+        assert torch.equal(exact, out_ref)
+    assert rel_err(res[0][0][:, 12:].numpy(), out_ref.numpy()) <= TOL
+    assert rel_err(res[1][0][:, 12:].numpy(), out_ref.numpy()) <= TOL
     assert rel_err(res[0][1].numpy(), (dx_ref + G).numpy()) <= TOL
     dz_ref = dgb_ref * torch.sigmoid(z) * (1 - torch.sigmoid(z))
     assert rel_err(res[0][2].numpy(), dz_ref.numpy()) <= TOL
