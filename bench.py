@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""Benchmark: aggregated node-features/sec through one GCN layer (BASELINE.json ``metric``).
+"""Benchmark: aggregated node-features/sec through the GCN (BASELINE.json ``metric``).
 
-Workload (SURVEY.md §8(d) north-star target): per rank B=32 per-frame graphs of N=8 robots
+Headline workload (SURVEY.md §8(d) north-star target): per rank B=32 per-frame graphs of N=8 robots
 (complete directed graphs, the reference's ``dgl/dataloader.py:88-95``), node features
 C=512 x 32 x 32 fp32 (ResNet18 width at H/8 x W/8 of a 256^2 image), synthetic and seeded, already
-resident in HBM.  A *step* is one forward pass of the drop-in ``GCN`` layer over that batch:
-edge encoder (9 -> C -> 2C Linear/ReLU/Linear/Sigmoid on the 1792 edge poses: HIP hidden-layer
-kernel + library GEMM) + the HIP FiLM-mean aggregation (which applies the encoder's sigmoid).  value = elements (Nt*C*H*W) aggregated per second over all ranks.
+resident in HBM.  A *step* is one forward pass of the drop-in ``GCN`` layer over that batch: edge
+encoder (9 -> C -> 2C Linear/ReLU/Linear on the 1792 edge poses: HIP hidden-layer kernel + library
+GEMM) + the HIP FiLM-mean aggregation (which applies the encoder's sigmoid).  value = elements
+(Nt*C*H*W) aggregated per second over all ranks.
 
 Multi-GPU (``torch.distributed.run``, one process per GPU): graphs of a batch are independent, so
 each rank runs its own B=32 graphs with no data-path collective ("scaling": "weak"); time is the
@@ -17,8 +18,14 @@ Extra JSON fields:
   launches; achieved = algorithmic bytes per launch / mean launch time (bytes: DESIGN.md §4).
   ``traffic`` is the PMC-measured HBM bytes per launch (rocprofv3 FETCH_SIZE/WRITE_SIZE, corrected
   per MI355X_MICROARCH.md) when ``profiles/pmc_traffic_*.json`` for this workload exists, else null.
+* ``configs`` — one record per BASELINE.json config (configs[1..4]): the config's GCN stack (layers,
+  1x1 compress, k-NN graphs) forward and training step, and the roofline of its own forward and
+  backward aggregation kernels, timed over rotating buffer sets larger than the 256 MB Infinity
+  Cache.  configs[3] and [4] are data-parallel configs: with N > 1 ranks their global batch (32 and
+  64 graphs) is split over the ranks (``dist.shard_graph``, "strong"), and the training step
+  all-reduces the gradients over RCCL; with one rank they run the per-GPU share (8 graphs).
 * ``cpu_baseline`` — the CPU oracle (a torch restatement of the reference DGL UDF path, same op
-  sequence) on a bounded sample of the same workload, rank 0 at N=1 only.
+  sequence) on the headline workload, rank 0 at N=1 only, bounded in time.
 """
 from __future__ import annotations
 
@@ -26,8 +33,10 @@ import argparse
 import glob
 import json
 import os
+import platform
 import sys
 import time
+import types
 
 import numpy as np
 import torch
@@ -37,23 +46,42 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import mrp_gnn_amd as mrp  # noqa: E402
-from mrp_gnn_amd.dist import env_rank_world  # noqa: E402
+from mrp_gnn_amd.dist import GradAllReducer, env_rank_world, shard_graph  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+MALL_BYTES = 256 << 20  # Infinity Cache: rotating buffer sets must exceed 2x this
 METRIC = "aggregated node-features/sec (N×C×H×W elems through GCN) at 1/2/4/8 MI355X"
 
+# BASELINE.json configs[1..4] (configs[0] is the reference's CPU-only case: cpu_baseline).
+# SURVEY.md §8(d) fixes the shapes; "per_gpu" is the graphs one GPU holds in the config.
+CONFIGS = {
+    1: dict(name="configs[1]: 8-robot warehouse, ResNet18 512 x H/8 x W/8 (32x32), 2-layer GCN "
+                 "(multi_gcn + compress), batch 16, 1 GPU",
+            batch=16, per_gpu=16, N=8, C=512, H=32, layers=2, knn=None, split=False),
+    2: dict(name="configs[2]: 8-robot airsim, gcn_compress (FiLM e_mul_u, 1x1 compress), MobileNetV2 "
+                 "1280 x 8x8, batch 32, 1 GPU",
+            batch=32, per_gpu=32, N=8, C=1280, H=8, layers=1, knn=None, split=False),
+    3: dict(name="configs[3]: 8-robot warehouse, ResNet50 2048 x 8x8, 2-layer GCN (multi_gcn + compress; "
+                 "GCN2Conv mapped per SURVEY §8(d)), batch 32, DP over 4 GPUs",
+            batch=32, per_gpu=8, N=8, C=2048, H=8, layers=2, knn=None, split=True),
+    4: dict(name="configs[4]: 16-robot synthetic k-NN(4), 1024 x 16x16, 3 GCN layers, batch 64, DP over 8 "
+                 "GPUs with RCCL gradient all-reduce",
+            batch=64, per_gpu=8, N=16, C=1024, H=16, layers=3, knn=4, split=True),
+}
 
-def make_workload(B, N, C, H, W, seed, device):
+
+def make_workload(B, N, C, H, W, seed, device, knn=None, features=True):
     rng = np.random.RandomState(seed)
     graphs = []
     for _ in range(B):
         t = rng.uniform(-10, 10, size=(N, 3))
         q = rng.standard_normal((N, 4))
         q /= np.linalg.norm(q, axis=1, keepdims=True)
-        graphs.append(mrp.frame_graph(np.concatenate([t, q], 1).astype(np.float32)))
+        graphs.append(mrp.frame_graph(np.concatenate([t, q], 1).astype(np.float32), knn=knn))
     g = mrp.batch(graphs)
-    gen = torch.Generator().manual_seed(seed)
-    g.ndata["image"] = torch.randn(B * N, C, H, W, generator=gen)
+    if features:
+        gen = torch.Generator().manual_seed(seed)
+        g.ndata["image"] = torch.randn(B * N, C, H, W, generator=gen)
     return g.to(device)
 
 
@@ -63,29 +91,67 @@ def alg_bytes_fwd(Nt, E, C, P):
     return Nt * C * P * 4 + E * 2 * C * 4 + Nt * C * P * 4
 
 
-def time_kernel(x, gb, csr, out, iters, device):
-    """Mean duration of one aggregation launch, HIP events on the launch stream."""
+def alg_bytes_bwd(Nt, E, C, P):
+    """Backward (dx + d gamma/beta): grad_out and x read once, gamma/beta read once, dx written once,
+    d gamma/beta written once."""
+    return 2 * Nt * C * P * 4 + E * 2 * C * 4 + Nt * C * P * 4 + E * 2 * C * 4
+
+
+def time_launches(launches, iters, device):
+    """Mean duration of one launch, HIP events on the launch stream; ``launches`` are closures over
+    distinct buffer sets, run round-robin.  The ``iters`` launches are captured once in a HIP graph
+    and the events bracket its replay, so a short kernel is timed back to back on the device rather
+    than at the rate Python can issue ctypes calls (~15-20 us per call: more than a small config's
+    whole kernel)."""
+    for f in launches * 2:
+        f()
+    torch.cuda.synchronize(device)
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=side):
+        for i in range(iters):
+            launches[i % len(launches)]()
+    graph.replay()  # warm
+    torch.cuda.synchronize(device)
     stream = torch.cuda.current_stream(device)
-    mode = mrp._lib.MODE_FILM_MEAN | mrp._lib.GB_LOGITS
-    for _ in range(3):
-        mrp.film_mean_forward_into(x, gb, csr, mode, out)
     start = torch.cuda.Event(enable_timing=True)
     end = torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(device)
     start.record(stream)
-    for _ in range(iters):
-        mrp.film_mean_forward_into(x, gb, csr, mode, out)
+    graph.replay()
     end.record(stream)
     end.synchronize()
+    del graph
     return start.elapsed_time(end) / iters * 1e-3  # seconds
 
 
-def cpu_baseline(N, C, H, W, seconds, sample_graphs):
+def roofline(kernel, bytes_launch, t, traffic=None, traffic_src=None, **extra):
+    achieved = bytes_launch / t / 1e9
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+         "traffic": traffic, "kernel": kernel, "kernel_us": t * 1e6, "alg_bytes_per_launch": bytes_launch}
+    if traffic_src:
+        r["traffic_source"] = traffic_src
+    r.update(extra)
+    return r
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(B, N, C, H, W, seconds):
     """The reference op sequence on the host (oracle: edge encoder -> gather -> FiLM -> degree
-    bucket -> mean), bounded to about ``seconds`` of CPU work."""
+    bucket -> mean) over the headline workload itself, bounded to about ``seconds`` of CPU work."""
     import oracle
     threads = torch.get_num_threads()
-    g = make_workload(sample_graphs, N, C, H, W, seed=1234, device="cpu")
+    g = make_workload(B, N, C, H, W, seed=1234, device="cpu")
     torch.manual_seed(0)
     enc = mrp.edge_encoder([C, C])
     params = dict(enc.named_parameters())
@@ -94,7 +160,6 @@ def cpu_baseline(N, C, H, W, seconds, sample_graphs):
     pose = g.edata["pose"]
     elems = x.numel()
     with torch.no_grad():
-        oracle.gcn_forward(params, x, pose, src, dst)  # warm-up
         reps, t0 = 0, time.perf_counter()
         while True:
             oracle.gcn_forward(params, x, pose, src, dst)
@@ -103,8 +168,9 @@ def cpu_baseline(N, C, H, W, seconds, sample_graphs):
             if el >= seconds:
                 break
     return {"value": elems * reps / el, "unit": "elems/s", "cores": threads, "kind": "port",
-            "sample": f"{sample_graphs} graphs x N={N} x C={C} x {H}x{W}, {reps} forward passes in {el:.1f} s, "
-                      f"torch CPU fp32, {threads} threads"}
+            "cpu": cpu_model(),
+            "sample": f"the headline workload itself ({B} graphs x N={N} x C={C} x {H}x{W}), {reps} forward "
+                      f"passes in {el:.1f} s, torch CPU fp32, {threads} threads"}
 
 
 def graph_build_time(B, N, device, reps=20):
@@ -136,7 +202,7 @@ def graph_build_time(B, N, device, reps=20):
             "device_us": dev_s * 1e6, "host_us": host_s * 1e6}
 
 
-def pmc_traffic(workload):
+def pmc_traffic(workload, kernel="film_fwd"):
     """Per-launch HBM bytes from a committed rocprofv3 PMC summary for this workload, if any."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_*.json")))
     for f in reversed(files):
@@ -144,8 +210,9 @@ def pmc_traffic(workload):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("workload") == workload and d.get("kernel") == "film_fwd":
-            return d.get("hbm_bytes_per_launch"), os.path.basename(f)
+        for rec in d if isinstance(d, list) else [d]:
+            if rec.get("workload") == workload and rec.get("kernel") == kernel:
+                return rec.get("hbm_bytes_per_launch"), os.path.basename(f)
     return None, None
 
 
@@ -157,10 +224,23 @@ def max_over_ranks(seconds, world, device, backend):
     return float(t.item())
 
 
+def timed(fn, steps, world, device, backend):
+    """Barrier + synchronize on both sides of ``steps`` calls; max over ranks (seconds per call)."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    return max_over_ranks((time.perf_counter() - t0) / steps, world, device, backend)
+
+
 def train_step_time(gcn, g, x, world, device, args):
     """One training step of the layer: forward, backward through the HIP kernels and the edge
     encoder, and (N > 1) the bucketed gradient all-reduce of the replicated parameters."""
-    from mrp_gnn_amd.dist import GradAllReducer
     xr = x.detach().clone().requires_grad_(True)
     grad = torch.randn_like(x)
     reducer = GradAllReducer(gcn.parameters()) if world > 1 else None
@@ -175,49 +255,109 @@ def train_step_time(gcn, g, x, world, device, args):
 
     for _ in range(3):
         step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for _ in range(args.train_steps):
-        step()
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    t = max_over_ranks((time.perf_counter() - t0) / args.train_steps, world, device, args.dist_backend)
+    t = timed(step, args.train_steps, world, device, args.dist_backend)
     nb = len(reducer.buckets) if reducer is not None else 0
     if reducer is not None:
         reducer.remove()
     return t, nb
 
 
-def block_step_time(world, device, args, rank):
-    """BASELINE configs[1]: the 2-layer GCN of multi_view_dgl_model (compress_gcn + multi_gcn:
-    gcn1 -> cat -> conv1 -> gcn2 -> cat -> conv2, dgl/model/models.py:180-189) on B=16 8-robot
-    graphs, 512 x 32 x 32 features, forward.  Reported beside the north-star line, not as value."""
-    B, N, C, H = 16, 8, 512, 32
-    g = make_workload(B, N, C, H, H, seed=100 + rank, device=device)
-    opt = type("opt", (), {"feature_dim": C, "compress_gcn": True, "multi_gcn": True})()
+def rotating_sets(set_bytes, min_total=2 * MALL_BYTES + (128 << 20), max_sets=64):
+    """How many buffer sets of ``set_bytes`` to rotate so the timed launches stream from HBM."""
+    return max(1, min(max_sets, -(-min_total // max(set_bytes, 1))))
+
+
+def config_record(cid, world, rank, device, args):
+    """One BASELINE config: its GCN stack's forward and training step, and the roofline of its own
+    forward and backward aggregation kernels over rotating buffers."""
+    cfg = CONFIGS[cid]
+    N, C, H, layers, knn = cfg["N"], cfg["C"], cfg["H"], cfg["layers"], cfg["knn"]
+    P = H * H
+    if cfg["split"] and world > 1:
+        # the global batch's frames on every rank (cheap), this rank's share of them with features
+        glob_g = make_workload(cfg["batch"], N, C, H, H, seed=300 + cid, device="cpu", knn=knn, features=False)
+        g, (lo, hi) = shard_graph(glob_g, rank, world)
+        gen = torch.Generator().manual_seed(1000 * cid + lo)
+        g.ndata["image"] = torch.randn(g.num_nodes(), C, H, H, generator=gen)
+        g = g.to(device)
+        scaling, share = "strong", f"graphs [{lo}, {hi}) of {cfg['batch']}"
+    else:
+        B = cfg["per_gpu"] if cfg["split"] else cfg["batch"]
+        g = make_workload(B, N, C, H, H, seed=300 + cid + 17 * rank, device=device, knn=knn)
+        lo, hi = 0, B
+        scaling = "weak"
+        share = f"{B} graphs per rank" + (f" (the per-GPU share of {cfg['batch']})" if cfg["split"] else "")
+    opt = types.SimpleNamespace(feature_dim=C, compress_gcn=True, multi_gcn=False, gcn_layers=layers,
+                                gcn_combine="cat_compress")
     torch.manual_seed(0)
-    block = mrp.GCNBlock(opt).to(device)
+    net = mrp.GCNStack(opt).to(device)
     x = g.ndata["image"]
+    Nt, E = g.num_nodes(), g.num_edges()
+    csr = g.csr(device)
+    elems = layers * Nt * C * P  # node features through the GCN layers per step (this rank)
+    rec = {"config": cfg["name"], "graphs_per_rank": hi - lo, "share": share, "robots": N, "channels": C,
+           "H": H, "W": H, "layers": layers, "graph": f"k-NN({knn})" if knn else "complete",
+           "graph_kind": "regular" if knn else "complete", "scaling": scaling}
     with torch.no_grad():
+        fwd = lambda: net(g, x)  # noqa: E731
         for _ in range(3):
-            block(g, x)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        for _ in range(args.block_steps):
-            block(g, x)
-        torch.cuda.synchronize(device)
-        if world > 1:
-            dist.barrier()
-    t = max_over_ranks((time.perf_counter() - t0) / args.block_steps, world, device, args.dist_backend)
-    elems = 2 * g.num_nodes() * C * H * H  # two GCN layers
-    return {"config": "configs[1]: B=16/rank, N=8 complete, C=512, 32x32, 2 GCN layers with 1x1 compress "
-                      "(gcn1-cat-conv1-gcn2-cat-conv2), forward",
-            "value": world * elems / t, "unit": "elems/s", "ms_per_step": t * 1e3}
+            fwd()
+        t = timed(fwd, args.config_steps, world, device, args.dist_backend)
+    rec["forward"] = {"value": world * elems / t if scaling == "weak" else None, "unit": "elems/s",
+                      "ms_per_step": t * 1e3}
+    if scaling == "strong":  # every rank holds a different part of one global batch
+        tot = torch.tensor([float(elems)], dtype=torch.float64,
+                           device=device if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(tot)
+        rec["forward"]["value"] = float(tot.item()) / t
+    # training step: forward + backward (+ RCCL gradient all-reduce, weighted by shard size)
+    xr = x.detach().clone().requires_grad_(True)
+    gy = torch.randn(Nt, C, H, H, device=device)
+    reducer = GradAllReducer(net.parameters()) if world > 1 else None
+    if reducer is not None:
+        reducer.set_local_count(hi - lo)
+
+    def train():
+        for p in net.parameters():
+            p.grad = None
+        net(g, xr).backward(gy)
+        if reducer is not None:
+            reducer.synchronize()
+
+    for _ in range(2):
+        train()
+    tt = timed(train, args.config_steps, world, device, args.dist_backend)
+    rec["train_step"] = {"value": rec["forward"]["value"] * t / tt, "unit": "elems/s", "ms_per_step": tt * 1e3,
+                         "allreduce": (f"{len(reducer.buckets)} bucket(s), {sum(p.numel() for p in net.parameters()) * 4 / 2**20:.1f} MiB"
+                                       if reducer is not None else None)}
+    if reducer is not None:
+        reducer.remove()
+    # kernel rooflines on rotating buffer sets (layer 1's aggregation: the kernels every layer runs)
+    with torch.no_grad():
+        z = net.gcn1.edge_encoder.logits(g.edata["pose"])
+    mode = mrp._lib.MODE_FILM_MEAN | mrp._lib.GB_LOGITS
+    plane = Nt * C * P * 4
+    nf = rotating_sets(2 * plane + E * 2 * C * 4)
+    sets = [(x if i == 0 else torch.randn_like(x), torch.empty_like(x)) for i in range(nf)]
+    launches = [lambda xi=xi, oi=oi: mrp.film_mean_forward_into(xi, z, csr, mode, oi) for xi, oi in sets]
+    tf = time_launches(launches, args.kernel_iters, device)
+    kname = "film_fwd_regular" if knn else "film_fwd"
+    rec["roofline_fwd"] = roofline(kname, alg_bytes_fwd(Nt, E, C, P), tf, rotating_sets=nf,
+                                   footprint_mb=round(nf * (2 * plane) / 2**20))
+    del sets, launches
+    nb = rotating_sets(3 * plane + 2 * E * 2 * C * 4)
+    bsets = [(torch.randn_like(x), x if i == 0 else torch.randn_like(x)) for i in range(nb)]
+
+    def bwd(G, xi):
+        return mrp.aggregate.film_mean_backward(G, xi, z, csr, mode, True, True)
+
+    launches = [lambda G=G, xi=xi: bwd(G, xi) for G, xi in bsets]
+    tb = time_launches(launches, args.kernel_iters, device)
+    bname = ("film_bwd_regular" if knn and N > 8 else "film_bwd_fused")
+    rec["roofline_bwd"] = roofline(bname, alg_bytes_bwd(Nt, E, C, P), tb, rotating_sets=nb,
+                                   footprint_mb=round(nb * (3 * plane) / 2**20))
+    del bsets, launches
+    return rec
 
 
 def main():
@@ -233,12 +373,11 @@ def main():
     ap.add_argument("--spinup-s", type=float, default=0.5,
                     help="untimed back-to-back steps before the warmup steps (GPU clock ramp from idle)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-sample-graphs", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step measurement")
     ap.add_argument("--train-steps", type=int, default=20)
-    ap.add_argument("--no-block", action="store_true", help="skip the configs[1] 2-layer block measurement")
-    ap.add_argument("--block-steps", type=int, default=10)
+    ap.add_argument("--configs", default="1,2,3,4", help="BASELINE configs to measure ('' for none)")
+    ap.add_argument("--config-steps", type=int, default=10)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (control-flow tests)")
     args = ap.parse_args()
 
@@ -256,7 +395,7 @@ def main():
     P = H * W
     workload = f"gcn_film_mean_fwd_B{B}_N{N}_complete_C{C}_{H}x{W}_fp32"
     g = make_workload(B, N, C, H, W, seed=rank, device=device)
-    opt = type("opt", (), {"feature_dim": C})()
+    opt = types.SimpleNamespace(feature_dim=C)
     torch.manual_seed(0)
     gcn = mrp.GCN(opt).to(device)
     x = g.ndata["image"]
@@ -280,35 +419,26 @@ def main():
             spin_steps += 20
         for _ in range(args.warmup):
             step()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize(device)
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        elapsed = max_over_ranks(elapsed, world, device, args.dist_backend)
+        elapsed = timed(step, args.steps, world, device, args.dist_backend) * args.steps
 
         # dominant kernel alone, for the roofline
         z = gcn.edge_encoder.logits(g.edata["pose"])  # what GCN.forward hands the kernel
         out = torch.empty_like(x)
-        t_kernel = time_kernel(x, z, csr, out, args.kernel_iters, device)
+        mode = mrp._lib.MODE_FILM_MEAN | mrp._lib.GB_LOGITS
+        t_kernel = time_launches([lambda: mrp.film_mean_forward_into(x, z, csr, mode, out)], args.kernel_iters,
+                                 device)
 
-    train = None
-    if not args.no_train:
-        train = train_step_time(gcn, g, x, world, device, args)
-    block = None if args.no_block else block_step_time(world, device, args, rank)
+    train = None if args.no_train else train_step_time(gcn, g, x, world, device, args)
+    configs = {}
+    for cid in [int(c) for c in args.configs.split(",") if c.strip()]:
+        configs[f"configs[{cid}]"] = config_record(cid, world, rank, device, args)
+        torch.cuda.empty_cache()
     gbuild = graph_build_time(B, N, device)
 
     elems_per_step = Nt * C * P
     value = world * elems_per_step * args.steps / elapsed
     bytes_launch = alg_bytes_fwd(Nt, E, C, P)
-    achieved = bytes_launch / t_kernel / 1e9
     traffic, traffic_src = pmc_traffic(workload)
-
     result = {
         "metric": METRIC,
         "value": value,
@@ -326,11 +456,8 @@ def main():
         "data": "synthetic (seeded complete 8-robot graphs, relative poses from random robot poses, randn features)",
         "config": {"workload": workload, "graphs_per_rank": B, "global_graphs": B * world, "robots": N,
                    "channels": C, "H": H, "W": W, "layers": 1, "parallelism": f"dp{world} (independent graphs)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "film_fwd",
-                     "kernel_us": t_kernel * 1e6, "alg_bytes_per_launch": bytes_launch,
-                     "read_frac": (bytes_launch - Nt * C * P * 4) / t_kernel / 1e9 / HBM_PEAK_GBS,
-                     "traffic_source": traffic_src},
+        "roofline": roofline("film_fwd", bytes_launch, t_kernel, traffic, traffic_src,
+                             read_frac=(bytes_launch - Nt * C * P * 4) / t_kernel / 1e9 / HBM_PEAK_GBS),
     }
     if train is not None:
         t_train, reducer_buckets = train
@@ -340,11 +467,11 @@ def main():
             "value": world * elems_per_step / t_train, "unit": "elems/s", "ms_per_step": t_train * 1e3,
             "allreduce_buckets": reducer_buckets,
         }
-    if block is not None:
-        result["block_step"] = block
+    if configs:
+        result["configs"] = configs
     result["graph_build"] = gbuild
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(N, C, H, W, args.cpu_seconds, args.cpu_sample_graphs)
+        result["cpu_baseline"] = cpu_baseline(B, N, C, H, W, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -194,7 +194,11 @@ int mrp_film_mean_fwd_ex(const float* x, int64_t x_node_stride,
                          const mrp_agg_epilogue* epilogue,
                          void* stream);
 
-/* mrp_film_mean_bwd for a forward run with `epilogue` (NULL: plain; see mrp_agg_epilogue). */
+/* mrp_film_mean_bwd for a forward run with `epilogue` (NULL: plain; see mrp_agg_epilogue).
+ * workspace: optional device scratch of workspace_bytes >= mrp_film_mean_bwd_workspace(...) bytes
+ * (NULL/0 allowed).  For MRP_GRAPH_REGULAR graphs of more than 8 nodes it lets the backward split
+ * each channel plane over several workgroups and reduce their partial d gamma/beta sums in a second
+ * pass (fixed order: deterministic); without it each plane is one workgroup. */
 int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride,
                          const float* x, int64_t x_node_stride,
                          const float* gb,
@@ -206,7 +210,12 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride,
                          const float* grad_x_base, int64_t base_node_stride,
                          float* grad_gb,
                          const mrp_agg_epilogue* epilogue,
+                         void* workspace, int64_t workspace_bytes,
                          void* stream);
+
+/* Bytes of workspace mrp_film_mean_bwd_ex can use for these graph/feature sizes (0: none needed). */
+int64_t mrp_film_mean_bwd_workspace(int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
+                                    int32_t C, int32_t P);
 
 /*
  * First layer of the edge encoder, dgl/model/models.py:147-148:  h = relu(pose W1^T + b1).

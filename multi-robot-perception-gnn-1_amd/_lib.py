@@ -24,6 +24,7 @@ EXPORTED_SYMBOLS = (
     "mrp_film_mean_bwd",
     "mrp_film_mean_fwd_ex",
     "mrp_film_mean_bwd_ex",
+    "mrp_film_mean_bwd_workspace",
     "mrp_edge_hidden_fwd",
     "mrp_edge_encoder_bwd_workspace",
     "mrp_edge_encoder_bwd",
@@ -79,8 +80,10 @@ def _declare(lib: ctypes.CDLL) -> None:
     ep = ctypes.POINTER(Epilogue)
     lib.mrp_film_mean_fwd_ex.argtypes = [_P, _I64, _P] + graph + [_P, _I64, ep, _P]
     lib.mrp_film_mean_fwd_ex.restype = ctypes.c_int
-    lib.mrp_film_mean_bwd_ex.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _I64, _P, ep, _P]
+    lib.mrp_film_mean_bwd_ex.argtypes = [_P, _I64, _P, _I64, _P] + graph + [_P, _I64, _P, _I64, _P, ep, _P, _I64, _P]
     lib.mrp_film_mean_bwd_ex.restype = ctypes.c_int
+    lib.mrp_film_mean_bwd_workspace.argtypes = [_I32, _I32, _I32, _I32, _I32]
+    lib.mrp_film_mean_bwd_workspace.restype = ctypes.c_int64
     lib.mrp_tuning_set.argtypes = [ctypes.c_char_p, _I32]
     lib.mrp_tuning_set.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]

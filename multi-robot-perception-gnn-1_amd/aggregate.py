@@ -175,13 +175,19 @@ def film_mean_backward(grad_out: torch.Tensor, x: torch.Tensor, gb: Optional[tor
     if epilogue is not None and (epilogue.agg_scale != 1.0 or epilogue.self_scale != 0.0):
         ep = _lib.Epilogue(epilogue.agg_scale, epilogue.self_scale, 0, 0, 0.0, 0, 0)
     lib = _lib.load_library()
+    ws = None
+    if need_dgb:  # scratch for the plane-split k-NN backward (the library never allocates)
+        nbytes = int(lib.mrp_film_mean_bwd_workspace(csr.num_graphs, csr.max_nodes, csr.graph_kind, C, H * W))
+        if nbytes > 0:
+            ws = torch.empty(nbytes // 4 + 1, device=x.device, dtype=torch.float32)
     with torch.cuda.device(x.device):
         code = lib.mrp_film_mean_bwd_ex(
             _ptr(grad_out), gs, _ptr(x), xs, _ptr(gb), _ptr(csr.indptr), _ptr(csr.src), _ptr(csr.eid),
             _ptr(csr.graph_off), csr.num_graphs, csr.max_nodes, csr.graph_kind, csr.num_nodes, csr.num_edges, C,
             H * W, mode,
             _ptr(dx), (C * H * W) if dx is not None else 0, _ptr(grad_x_base), bs, _ptr(dgb),
-            ctypes.byref(ep) if ep is not None else None, _stream(x.device))
+            ctypes.byref(ep) if ep is not None else None, _ptr(ws), ws.numel() * 4 if ws is not None else 0,
+            _stream(x.device))
     _lib.check(code, "mrp_film_mean_bwd_ex")
     return dx, dgb
 

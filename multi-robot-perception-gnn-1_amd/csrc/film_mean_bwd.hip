@@ -7,6 +7,26 @@ using namespace mrp_host;
 
 namespace {
 
+// Geometry of film_bwd_regular (N > 8, uniform in-degree k <= 8) for slice width vec.
+Geometry regular_geometry(int C, int P, int vec) {
+  const Tuning& tu = tuning();
+  return vec == 2 ? make_geometry(C, P, 2, tu.bwd_regular_lanes, tu.bwd_regular_lanes, mrp::kMaxChanPerBlock)
+                  : make_geometry(C, P, 1, 2 * tu.bwd_regular_lanes, 2 * tu.bwd_regular_lanes, mrp::kMaxChanPerBlock);
+}
+
+// Plane segments of the split regular backward: each lane owns tu.bwd_regular_slices slices.
+int regular_psplit(const Geometry& g, int P) {
+  const int spl = tuning().bwd_regular_slices;
+  if (spl <= 0) return 1;
+  const int per_lane = (P / g.vec + g.lpc - 1) / g.lpc;
+  return std::max(1, per_lane / spl);
+}
+
+int64_t regular_ws_bytes(const Geometry& g, int num_graphs, int nt, int kmax, int psplit) {
+  return psplit <= 1 ? 0
+                     : (int64_t)num_graphs * g.ncb * psplit * g.cpb * (nt * kmax + nt) * (int64_t)sizeof(float);
+}
+
 hipError_t dispatch_bwd(int nt, bool complete, const AggArgs& a, const Geometry& g, hipStream_t st) {
   if (nt >= 1 && nt <= 8) return dispatch_bwd_1_8(nt, complete, a, g, st);
   if (nt >= 9 && nt <= 12) return dispatch_bwd_9_12(nt, complete, a, g, st);
@@ -26,7 +46,20 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
                       void* stream) {
   return mrp_film_mean_bwd_ex(grad_out, g_node_stride, x, x_node_stride, gb, indptr, src, eid, graph_off, num_graphs,
                               max_nodes, graph_kind, num_nodes, num_edges, C, P, mode_flags, grad_x, gx_node_stride,
-                              grad_x_base, base_node_stride, grad_gb, nullptr, stream);
+                              grad_x_base, base_node_stride, grad_gb, nullptr, nullptr, 0, stream);
+}
+
+int64_t mrp_film_mean_bwd_workspace(int32_t num_graphs, int32_t max_nodes, int32_t graph_kind, int32_t C, int32_t P) {
+  const int kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
+  if (num_graphs <= 0 || max_nodes <= 8 || max_nodes > MRP_MAX_NODES || kdeg < 1 || kdeg > 8 || C <= 0 || P <= 0)
+    return 0;
+  const int kmax = kdeg <= 4 ? 4 : 8;
+  int64_t bytes = 0;
+  for (int vec : {1, 2}) {  // the launch picks the slice width from pointer alignment: cover both
+    const Geometry g = regular_geometry(C, P, vec);
+    bytes = std::max(bytes, regular_ws_bytes(g, num_graphs, max_nodes, kmax, regular_psplit(g, P)));
+  }
+  return bytes;
 }
 
 int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const float* x, int64_t x_node_stride,
@@ -34,7 +67,8 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const flo
                          const int32_t* graph_off, int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
                          int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode_flags,
                          float* grad_x, int64_t gx_node_stride, const float* grad_x_base, int64_t base_node_stride,
-                         float* grad_gb, const mrp_agg_epilogue* ep, void* stream) {
+                         float* grad_gb, const mrp_agg_epilogue* ep, void* workspace, int64_t workspace_bytes,
+                         void* stream) {
   const float agg_scale = ep != nullptr ? ep->agg_scale : 1.f;
   const float self_scale = ep != nullptr ? ep->self_scale : 0.f;
   const int32_t logits = (mode_flags & MRP_AGG_GB_LOGITS) ? 1 : 0;
@@ -71,17 +105,25 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const flo
   if (max_nodes > 8 && kdeg >= 1 && kdeg <= 8) {
     // film_bwd_regular: 8-byte slices on 16 lanes per plane (367 us against 569 us on 64 lanes at
     // k-NN(4) N=16 C=1024 16x16): its prologue and lane reduction are amortised over more slices
-    vec = (vec4 && kdeg <= 4) ? 2 : 1;
-    g = vec == 2 ? make_geometry(C, P, 2, 16, 16, mrp::kMaxChanPerBlock)
-                 : make_geometry(C, P, 1, 32, 32, mrp::kMaxChanPerBlock);
+    const Tuning& tu = tuning();
+    vec = (vec4 && kdeg <= 4 && tu.bwd_regular_vec == 2) ? 2 : 1;
+    g = regular_geometry(C, P, vec);
   } else if (max_nodes <= 8) {
     // film_bwd_fused: up to 128 lanes (two waves) per plane, two slices per lane: 283 vs 306 us at
     // 64 lanes at the bench size (tools/fwd_lab.hip backward sweep; 256 lanes: 297 us)
-    g = make_geometry(C, P, vec, 8, 128, 32);
+    const Tuning& tu = tuning();
+    g = make_geometry(C, P, vec, tu.bwd_fused_lo, tu.bwd_fused_hi, tu.bwd_fused_cap);
   } else {
     g = make_geometry(C, P, vec, 64, 64, mrp::kMaxChanPerBlock);  // film_bwd_dx + Gram pass
   }
-  g.grid = (int64_t)num_graphs * g.ncb;
+  // REGULAR (k-NN) graphs with a large enough caller workspace: planes split over several workgroups,
+  // partial Grams reduced by a second kernel (film_bwd_regular_reduce)
+  int psplit = 1;
+  if (max_nodes > 8 && kdeg >= 1 && kdeg <= 8 && want_dgb && workspace != nullptr) {
+    const int ps = regular_psplit(g, P);
+    if (ps > 1 && regular_ws_bytes(g, num_graphs, max_nodes, kdeg <= 4 ? 4 : 8, ps) <= workspace_bytes) psplit = ps;
+  }
+  g.grid = (int64_t)num_graphs * g.ncb * psplit;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
   AggArgs a = {};
   a.x = x;
@@ -112,6 +154,8 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const flo
   a.agg_scale = agg_scale;
   a.self_scale = self_scale;
   a.epi = (agg_scale != 1.f || self_scale != 0.f) ? 1 : 0;
+  a.psplit = psplit;
+  a.ws = psplit > 1 ? static_cast<float*>(workspace) : nullptr;
   return dispatch_bwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, st);
 }
 

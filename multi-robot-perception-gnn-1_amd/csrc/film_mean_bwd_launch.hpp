@@ -49,13 +49,19 @@ template <int NT, int KMAX, bool DXB>
 hipError_t launch_bwd_regular(const AggArgs& a, const Geometry& g, hipStream_t st) {
   // VEC 4 would need 4*NT registers more per operand and spills; KMAX 8 only fits at VEC 1
   const size_t lds = lds_regular<NT, KMAX>(g.cpb);
+  bool done = false;
   if constexpr (KMAX <= 4) {
     if (g.vec == 2) {
       MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 2, DXB>), lds);
-      return hipGetLastError();
+      done = true;
     }
   }
-  MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 1, DXB>), lds);
+  if (!done) MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 1, DXB>), lds);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || a.psplit <= 1 || !a.want_dgb) return e;
+  // plane-split: add the segments' partial Grams (one workgroup per graph x channel block)
+  hipLaunchKernelGGL((mrp::film_bwd_regular_reduce<NT, KMAX>), dim3((unsigned)(g.grid / a.psplit)), dim3(mrp::kBlock), 0,
+                     st, a);
   return hipGetLastError();
 }
 

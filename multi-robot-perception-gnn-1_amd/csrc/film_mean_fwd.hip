@@ -43,10 +43,14 @@ hipError_t dispatch_fwd(int nt, bool complete, const AggArgs& a, const Geometry&
   MRP_DISPATCH_NT(nt, complete, launch_fwd_nt, a, g, st)
 }
 
-// REGULAR graphs: split the plane over workgroups like COMPLETE graphs (their prologue is two
-// rounds of loads, not a CSR walk).  An experiment knob (mrp_tuning_set).
-bool fwd_regular_split = true;
 }  // namespace
+
+namespace mrp_host {
+Tuning& tuning() {
+  static Tuning t;
+  return t;
+}
+}  // namespace mrp_host
 
 extern "C" {
 
@@ -54,9 +58,36 @@ int mrp_abi_version(void) { return 10; }
 
 int mrp_tuning_set(const char* name, int32_t value) {
   if (name == nullptr) return hipErrorInvalidValue;
-  if (std::strcmp(name, "fwd_regular_split") == 0) {
-    fwd_regular_split = value != 0;
+  Tuning& t = tuning();
+  if (std::strcmp(name, "reset") == 0) {
+    t = Tuning();
     return hipSuccess;
+  }
+  struct Knob {
+    const char* name;
+    int* field;
+    int lo, hi;
+  } knobs[] = {
+      {"fwd_lo", &t.fwd_lo, 1, 256},
+      {"fwd_hi", &t.fwd_hi, 1, 256},
+      {"fwd_cap", &t.fwd_cap, 1, 16},
+      {"fwd_regular_split", &t.fwd_regular_split, 0, 1},
+      {"fwd_regular_lo", &t.fwd_regular_lo, 1, 256},
+      {"fwd_regular_hi", &t.fwd_regular_hi, 1, 256},
+      {"fwd_regular_cap", &t.fwd_regular_cap, 1, 16},
+      {"bwd_fused_lo", &t.bwd_fused_lo, 1, 256},
+      {"bwd_fused_hi", &t.bwd_fused_hi, 1, 256},
+      {"bwd_fused_cap", &t.bwd_fused_cap, 1, 64},
+      {"bwd_regular_vec", &t.bwd_regular_vec, 1, 2},
+      {"bwd_regular_lanes", &t.bwd_regular_lanes, 1, 64},
+      {"bwd_regular_slices", &t.bwd_regular_slices, 0, 64},
+  };
+  for (const Knob& k : knobs) {
+    if (std::strcmp(name, k.name) == 0) {
+      if (value < k.lo || value > k.hi) return hipErrorInvalidValue;
+      *k.field = value;
+      return hipSuccess;
+    }
   }
   return hipErrorInvalidValue;
 }
@@ -94,13 +125,15 @@ int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const 
   const int32_t kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
   const bool regular = kdeg >= 1 && kdeg <= 8;
   // 16-byte slices beat 8-byte ones at every measured size (tools/kernel_lab.hip product sweep)
-  Geometry g = make_geometry(C, P, vec4 ? 4 : 1, 16, 64, mrp::kMaxChanPerBlock);
+  const Tuning& tu = tuning();
+  Geometry g = regular ? make_geometry(C, P, vec4 ? 4 : 1, tu.fwd_regular_lo, tu.fwd_regular_hi, tu.fwd_regular_cap)
+                       : make_geometry(C, P, vec4 ? 4 : 1, tu.fwd_lo, tu.fwd_hi, tu.fwd_cap);
   // COMPLETE graphs: one slice per lane, the plane split over ceil(PV / lpc) workgroups (their
   // prologue is one round of independent gamma/beta loads, hidden under the first slice).  CSR
   // graphs keep whole planes: their prologue walks the CSR (dependent loads) and a split repeats it
   // per segment (k-NN(4) N=16 C=1024 16x16: 304 us split vs 225 us whole)
   const int32_t pv = P / g.vec;
-  const int32_t psplit = (graph_kind == MRP_GRAPH_COMPLETE || (regular && fwd_regular_split))
+  const int32_t psplit = (graph_kind == MRP_GRAPH_COMPLETE || (regular && tu.fwd_regular_split))
                              ? (pv + g.lpc - 1) / g.lpc
                              : 1;
   g.grid = (int64_t)num_graphs * g.ncb * psplit;

@@ -78,6 +78,8 @@ struct AggArgs {
   float agg_scale, self_scale, x0_scale;
   const float* x0;
   int64_t x0s;
+  // backward of REGULAR graphs with psplit > 1: per-segment partial Grams, [graph][cb][seg][cpb][NS + NT]
+  float* ws;
 };
 
 // Forward epilogue of destination `node`, channel c, slice at `off` (see AggArgs::epi).
@@ -184,7 +186,11 @@ __device__ __forceinline__ float* at_bytes(float* base, uint32_t off) {
 template <int NT>
 struct Tile {
   static constexpr int NTP = (NT + 3) & ~3;  // padded row -> 16-byte aligned LDS rows
-  static constexpr int SZ = NT * NTP;        // floats per channel tile
+  // floats per channel tile, padded by 4: consecutive channels' tiles start 4 banks apart, so the
+  // channel groups of one wave (4-8 channels at 8x8 planes) read their broadcast weights without
+  // the 4-8-way LDS bank conflicts an unpadded 64- or 256-float stride gives (rocprof r02: 70 % of
+  // LDS cycles were conflicts at 8x8)
+  static constexpr int SZ = NT * NTP + 4;
 };
 
 // Edge id of u -> v (u != v) in a complete graph of n nodes whose edges start at ebase and are
@@ -538,11 +544,12 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
 template <int NT, int KMAX, int VEC>
 __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
   constexpr int NS = NT * KMAX;
+  constexpr int WS = NS + 2;     // per-channel stride of the slot weights (float2), padded 4 banks
   constexpr int WPD = KMAX / 4;  // 32-bit words of packed 8-bit slot sources per destination
   static_assert(KMAX % 4 == 0, "slots are packed four to a word");
   extern __shared__ float4 smem_f4[];
-  float2* Wl = reinterpret_cast<float2*>(smem_f4);                  // [cpb][NS] (gamma, beta) per slot
-  unsigned* slot_u = reinterpret_cast<unsigned*>(Wl + a.cpb * NS);  // [NT * WPD] packed local sources
+  float2* Wl = reinterpret_cast<float2*>(smem_f4);                  // [cpb][WS] (gamma, beta) per slot
+  unsigned* slot_u = reinterpret_cast<unsigned*>(Wl + a.cpb * WS);  // [NT * WPD] packed local sources
   int* slot_e = reinterpret_cast<int*>(slot_u + NT * WPD);          // [NS] edge id of the slot (-1: none)
 
   const int ps = a.psplit > 1 ? a.psplit : 1;
@@ -620,7 +627,7 @@ __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
         if (a.logits) w = make_float2(sigmoidf(w.x), sigmoidf(w.y));
       }
     }
-    Wl[cl * NS + slot] = w;
+    Wl[cl * WS + slot] = w;
   }
   __syncthreads();
   if (!active) return;
@@ -633,7 +640,7 @@ __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
     // every destination row is computed (full unroll); rows past the graph's nodes are not stored
 #pragma unroll
     for (int v = 0; v < NT; ++v) {
-      int wbase = grp * NS;  // laundered: weights stay in LDS (broadcast reads), not hoisted
+      int wbase = grp * WS;  // laundered: weights stay in LDS (broadcast reads), not hoisted
       asm volatile("" : "+v"(wbase));
       const float2* Wc = Wl + wbase;
       unsigned uw[WPD];
@@ -718,33 +725,39 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
   const int c = c0 + grp;
   if (grp >= a.cpb || c >= a.C) return;
 
-  const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c * a.P;
-  float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
+  // uniform bases, per-lane 32-bit byte offsets (at_bytes); slices as NT-wide vectors (no scratch)
+  const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c0 * a.P;
+  float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c0 * a.P;
+  const float* dxbase = a.dxb != nullptr ? a.dxb + (int64_t)node0 * a.dxbs + (int64_t)c0 * a.P : nullptr;
+  const uint32_t lane_plane = (uint32_t)grp * (uint32_t)a.P * 4u;
+  typedef float vnt __attribute__((ext_vector_type(NT <= 4 ? 4 : (NT <= 8 ? 8 : 16))));
 
   for (int j = li; j < a.PV; j += a.lpc) {
-    const int64_t off = (int64_t)j * VEC;
+    const uint32_t lane_off = lane_plane + (uint32_t)j * VEC * 4u;
     int tile = grp * SZ;  // laundered: keep the weights in LDS, not hoisted into registers
     asm volatile("" : "+v"(tile));
     const float* W = Wt + tile;
-    Frag<VEC> gv[NT];
+    vnt gv[VEC];
 #pragma unroll
     for (int v = 0; v < NT; ++v) {
       const int vv = v < n ? v : n - 1;
-      gv[v] = load_frag<VEC, true>(gbase + (int64_t)vv * a.gs + off);
+      const Frag<VEC> f = load_frag<VEC, true>(at_bytes(gbase + (int64_t)vv * a.gs, lane_off));
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) gv[k][v] = f.v[k];
     }
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
       if (!COMPLETE && u >= n) break;
       Frag<VEC> acc;
       if (DXB) {  // grad_x_base: a separate instantiation (it costs registers)
-        acc = load_frag<VEC, true>(a.dxb + (int64_t)(node0 + u) * a.dxbs + (int64_t)c * a.P + off);
+        acc = load_frag<VEC, true>(at_bytes(dxbase + (int64_t)u * a.dxbs, lane_off));
       } else {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
       }
       if (a.self_scale != 0.f) {  // residual epilogue: d out / d x[u] includes self_scale
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(a.self_scale, gv[u].v[k], acc.v[k]);
+        for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(a.self_scale, gv[k][u], acc.v[k]);
       }
 #pragma unroll
       for (int v4 = 0; v4 < NTP; v4 += 4) {
@@ -755,10 +768,10 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
           if (v >= NT) break;
           if (COMPLETE && v == u) continue;
 #pragma unroll
-          for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(w[q], gv[v].v[k], acc.v[k]);
+          for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(w[q], gv[k][v], acc.v[k]);
         }
       }
-      store_frag<VEC, true>(ob + (int64_t)u * a.os + off, acc);
+      store_frag<VEC, true>(at_bytes(ob + (int64_t)u * a.os, lane_off), acc);
     }
   }
 }
@@ -838,9 +851,12 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   const int c = c0 + grp;
   const bool active = grp < a.cpb && c < a.C;
 
-  const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c * a.P;
-  const float* xbase = a.x + (int64_t)node0 * a.xs + (int64_t)c * a.P;
-  float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
+  // uniform per-graph/channel-block bases, per-lane 32-bit byte offsets (see at_bytes)
+  const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c0 * a.P;
+  const float* xbase = a.x + (int64_t)node0 * a.xs + (int64_t)c0 * a.P;
+  float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c0 * a.P;
+  const float* dxbase = a.dxb != nullptr ? a.dxb + (int64_t)node0 * a.dxbs + (int64_t)c0 * a.P : nullptr;
+  const uint32_t lane_plane = (uint32_t)grp * (uint32_t)a.P * 4u;
   const bool do_dx = kOnePass && a.want_dx;
 
   // slice fragments: for the one-pass kernel the first slice is loaded before the prologue, so the
@@ -848,18 +864,18 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   Frag<VEC> gv[VB];
   Frag<VEC> xv[NT];
   auto load_slice = [&](int vb, int j) {
-    const int64_t off = (int64_t)j * VEC;
+    const uint32_t lane_off = lane_plane + (uint32_t)j * VEC * 4u;
 #pragma unroll
     for (int i = 0; i < VB; ++i) {
       const int v = vb + i;
       const int vv = v < n ? v : n - 1;
-      gv[i] = load_frag<VEC, kOnePass>(gbase + (int64_t)vv * a.gs + off);
+      gv[i] = load_frag<VEC, kOnePass>(at_bytes(gbase + (int64_t)vv * a.gs, lane_off));
     }
     if (a.want_dgb) {
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         const int uu = u < n ? u : n - 1;
-        xv[u] = load_frag<VEC, kOnePass>(xbase + (int64_t)uu * a.xs + off);
+        xv[u] = load_frag<VEC, kOnePass>(at_bytes(xbase + (int64_t)uu * a.xs, lane_off));
       }
     }
   };
@@ -889,7 +905,7 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
       int j = li;
       if (!kOnePass && j < a.PV) load_slice(vb, j);
       while (j < a.PV) {
-        const int64_t off = (int64_t)j * VEC;
+        const uint32_t lane_off = lane_plane + (uint32_t)j * VEC * 4u;
         int tile = grp * SZ;  // laundered: keep the weights in LDS, not hoisted into registers
         asm volatile("" : "+v"(tile));
         const float* W = Wt + tile;
@@ -899,7 +915,7 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
             if (!COMPLETE && u >= n) break;
             Frag<VEC> acc;
             if (DXB) {  // grad_x_base: a separate instantiation (it costs registers)
-              acc = load_frag<VEC, true>(a.dxb + (int64_t)(node0 + u) * a.dxbs + (int64_t)c * a.P + off);
+              acc = load_frag<VEC, true>(at_bytes(dxbase + (int64_t)u * a.dxbs, lane_off));
             } else {
 #pragma unroll
               for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
@@ -920,7 +936,7 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
                 for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(w[q], gv[v].v[k], acc.v[k]);
               }
             }
-            store_frag<VEC, true>(ob + (int64_t)u * a.os + off, acc);
+            store_frag<VEC, true>(at_bytes(ob + (int64_t)u * a.os, lane_off), acc);
           }
         }
         if (a.want_dgb) {
@@ -1050,13 +1066,60 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
   int* slot_u = reinterpret_cast<int*>(sc + NTP);  // [NS] local source of slot (v, j)
   int* slot_e = slot_u + NS;                       // [NS] edge id of slot (v, j)
 
-  const int b = blockIdx.x / a.ncb;
-  const int cb = blockIdx.x - b * a.ncb;
+  // psplit > 1: the plane is cut into segments, one workgroup each (4x the workgroups of whole
+  // planes, 2 slices per lane); each writes its partial Gram to a.ws and film_bwd_regular_reduce adds
+  // the segments in order (deterministic).  psplit == 1: the epilogue below writes d gamma/beta.
+  const int ps = a.psplit > 1 ? a.psplit : 1;
+  const int item = blockIdx.x / ps;
+  const int seg = blockIdx.x - item * ps;
+  const int b = item / a.ncb;
+  const int cb = item - b * a.ncb;
+  const int seglen = (a.PV + ps - 1) / ps;
+  const int jbeg = seg * seglen;
+  const int jend = min(a.PV, jbeg + seglen);
   const int node0 = a.goff[b];
   const int n = min(a.goff[b + 1] - node0, NT);
   if (n <= 0) return;
   const int c0 = cb * a.cpb;
   const int K = a.kdeg;
+
+  const int grp = threadIdx.x / a.lpc;
+  const int li = threadIdx.x - grp * a.lpc;
+  const int c = c0 + grp;
+  const bool active = grp < a.cpb && c < a.C;
+  // uniform per-graph/channel-block bases, per-lane 32-bit byte offsets (see at_bytes)
+  const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c0 * a.P;
+  const float* xbase = a.x + (int64_t)node0 * a.xs + (int64_t)c0 * a.P;
+  float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c0 * a.P;
+  const float* dxbase = a.dxb != nullptr ? a.dxb + (int64_t)node0 * a.dxbs + (int64_t)c0 * a.P : nullptr;
+  const uint32_t lane_plane = (uint32_t)grp * (uint32_t)a.P * 4u;
+
+
+  // slice registers; the first slice is loaded before the prologue (slots + transposed weight tiles:
+  // dependent loads) so that its latency hides under these loads
+  float gv[NT][VEC];
+  float xv[NT][VEC];
+  auto load_slice = [&](int jj) {
+    const uint32_t lane_off = lane_plane + (uint32_t)jj * VEC * 4u;
+#pragma unroll
+    for (int v = 0; v < NT; ++v) {
+      const int vv = v < n ? v : n - 1;
+      const Frag<VEC> f = load_frag<VEC, true>(at_bytes(gbase + (int64_t)vv * a.gs, lane_off));
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) gv[v][k] = f.v[k];
+    }
+    if (a.want_dgb) {
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        const int uu = u < n ? u : n - 1;
+        const Frag<VEC> f = load_frag<VEC, true>(at_bytes(xbase + (int64_t)uu * a.xs, lane_off));
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) xv[u][k] = f.v[k];
+      }
+    }
+  };
+  int j = jbeg + li;
+  if (active && j < jend) load_slice(j);
 
   for (int t = threadIdx.x; t < NS; t += blockDim.x) {
     const int v = t / KMAX, j = t - v * KMAX;
@@ -1073,14 +1136,6 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
   build_tiles_csr<NT, true>(a, node0, n, c0, Wt, nullptr, sc, nullptr);
   __syncthreads();
 
-  const int grp = threadIdx.x / a.lpc;
-  const int li = threadIdx.x - grp * a.lpc;
-  const int c = c0 + grp;
-  const bool active = grp < a.cpb && c < a.C;
-  const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c * a.P;
-  const float* xbase = a.x + (int64_t)node0 * a.xs + (int64_t)c * a.P;
-  float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
-
   float D[NS];
   float S[NT];
 #pragma unroll
@@ -1089,36 +1144,18 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
   for (int v = 0; v < NT; ++v) S[v] = 0.f;
 
   if (active) {
-    for (int j = li; j < a.PV; j += a.lpc) {
-      const int64_t off = (int64_t)j * VEC;
+    while (j < jend) {
+      const uint32_t lane_off = lane_plane + (uint32_t)j * VEC * 4u;
       int tile = grp * SZ;  // laundered: keep the weights in LDS, not hoisted into registers
       asm volatile("" : "+v"(tile));
       const float* W = Wt + tile;
-      float gv[NT][VEC];
-      float xv[NT][VEC];
-#pragma unroll
-      for (int v = 0; v < NT; ++v) {
-        const int vv = v < n ? v : n - 1;
-        const Frag<VEC> f = load_frag<VEC, true>(gbase + (int64_t)vv * a.gs + off);
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) gv[v][k] = f.v[k];
-      }
-      if (a.want_dgb) {
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-          const int uu = u < n ? u : n - 1;
-          const Frag<VEC> f = load_frag<VEC, true>(xbase + (int64_t)uu * a.xs + off);
-#pragma unroll
-          for (int k = 0; k < VEC; ++k) xv[u][k] = f.v[k];
-        }
-      }
       if (a.want_dx) {
 #pragma unroll
         for (int u = 0; u < NT; ++u) {
           if (u >= n) break;
           Frag<VEC> acc;
           if (DXB) {
-            acc = load_frag<VEC, true>(a.dxb + (int64_t)(node0 + u) * a.dxbs + (int64_t)c * a.P + off);
+            acc = load_frag<VEC, true>(at_bytes(dxbase + (int64_t)u * a.dxbs, lane_off));
           } else {
 #pragma unroll
             for (int k = 0; k < VEC; ++k) acc.v[k] = 0.f;
@@ -1138,7 +1175,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
               for (int k = 0; k < VEC; ++k) acc.v[k] = fmaf(w[q], gv[v][k], acc.v[k]);
             }
           }
-          store_frag<VEC, true>(ob + (int64_t)u * a.os + off, acc);
+          store_frag<VEC, true>(at_bytes(ob + (int64_t)u * a.os, lane_off), acc);
         }
       }
       if (a.want_dgb) {
@@ -1155,6 +1192,8 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
           }
         }
       }
+      j += a.lpc;
+      if (j < jend) load_slice(j);
     }
   }
   if (!a.want_dgb) return;
@@ -1176,6 +1215,16 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
     }
   }
   __syncthreads();
+  if (ps > 1) {
+    // partial Gram of this segment: [cpb][NS] then [cpb][NT], coalesced
+    float* w = a.ws + (int64_t)blockIdx.x * a.cpb * (NS + NT);
+    for (int t = threadIdx.x; t < a.cpb * NS; t += blockDim.x) w[t] = Dl[t];
+    for (int t = threadIdx.x; t < a.cpb * NT; t += blockDim.x) {
+      const int cl = t / NT, v = t - cl * NT;
+      w[a.cpb * NS + t] = Sl[cl * NTP + v];
+    }
+    return;
+  }
   // per-edge outputs: thread -> (channel fastest, slot)
   for (int t = threadIdx.x; t < a.cpb * NS; t += blockDim.x) {
     int cl, slot;
@@ -1187,6 +1236,46 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
     const float s = sc[v];
     const int64_t off = ((int64_t)e * a.C + cc) * 2;
     float2 r = make_float2(s * Dl[cl * NS + slot], s * Sl[cl * NTP + v]);
+    if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
+    *reinterpret_cast<float2*>(a.dgb + off) = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Second pass of the plane-split REGULAR backward: per (graph, channel block), add the psplit
+// partial Grams in segment order and write d gamma / d beta for every (edge slot, channel) —
+// the psplit == 1 epilogue of film_bwd_regular, reading partials from a.ws instead of LDS.
+// ---------------------------------------------------------------------------
+template <int NT, int KMAX>
+__global__ void __launch_bounds__(kBlock) film_bwd_regular_reduce(AggArgs a) {
+  constexpr int NS = NT * KMAX;
+  const int b = blockIdx.x / a.ncb;
+  const int cb = blockIdx.x - b * a.ncb;
+  const int node0 = a.goff[b];
+  const int n = min(a.goff[b + 1] - node0, NT);
+  if (n <= 0) return;
+  const int c0 = cb * a.cpb;
+  const int K = a.kdeg;
+  const int ps = a.psplit;
+  const float s = (a.mode != MRP_AGG_FILM_SUM ? 1.f / (float)K : 1.f) * a.agg_scale;
+  const float* w0 = a.ws + (int64_t)blockIdx.x * ps * a.cpb * (NS + NT);
+  for (int t = threadIdx.x; t < a.cpb * NS; t += blockDim.x) {
+    int cl, slot;
+    split_channel(a, t, cl, slot);
+    const int v = slot / KMAX, jj = slot - v * KMAX;
+    const int cc = c0 + cl;
+    if (v >= n || jj >= K || cc >= a.C) continue;
+    const int k = (node0 + v) * K + jj;  // REGULAR: v's CSR row is [K*v, K*(v+1))
+    const int u = a.src[k] - node0;
+    if ((unsigned)u >= (unsigned)n) continue;  // leaves the graph: rejected on the host
+    float dd = 0.f, ss = 0.f;
+    for (int sg = 0; sg < ps; ++sg) {
+      const float* w = w0 + (int64_t)sg * a.cpb * (NS + NT);
+      dd += w[cl * NS + slot];
+      ss += w[a.cpb * NS + cl * NT + v];
+    }
+    const int64_t off = ((int64_t)a.eid[k] * a.C + cc) * 2;
+    float2 r = make_float2(s * dd, s * ss);
     if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
     *reinterpret_cast<float2*>(a.dgb + off) = r;
   }
@@ -1205,6 +1294,27 @@ struct Geometry {
   int vec, lpc, cpb, threads, ncb;
   int64_t grid;
 };
+
+// Launch geometry knobs (defaults = the measured optima; mrp_tuning_set changes them for lab sweeps).
+struct Tuning {
+  int fwd_lo = 16, fwd_hi = 64, fwd_cap = 16;  // film_fwd: lanes per plane in [lo, hi], <= cap channels
+  // film_fwd_regular: whole planes, 32 lanes each (k-NN(4) N=16 C=1024 16x16, B=8: 54.1 us against
+  // 57.0 us split over 2 workgroups with 32 lanes; tools/sweep_geometry.py)
+  int fwd_regular_split = 0;
+  int fwd_regular_lo = 32, fwd_regular_hi = 32, fwd_regular_cap = 16;
+  // film_bwd_fused (N <= 8): at most 8 channels per workgroup — at 8x8 planes one-wave workgroups,
+  // 4x as many, so loads of later workgroups overlap the Gram reduction and epilogue of earlier
+  // ones (C=1280 B=32: 60.8 against 67.2 us with 32 channels; 32x32 planes are unaffected: 2)
+  int bwd_fused_lo = 8, bwd_fused_hi = 128, bwd_fused_cap = 8;
+  int bwd_regular_vec = 2, bwd_regular_lanes = 16;              // film_bwd_regular (N > 8, k-NN)
+  // film_bwd_regular: split planes so each lane owns this many slices (0: whole planes); needs the
+  // caller's workspace (mrp_film_mean_bwd_workspace), else whole planes.  Measured slower at the
+  // configs[4] shape (k-NN(4) N=16 C=1024 16x16 B=8: 102.7 us whole planes, 113 / 131 / 170 us at
+  // 4 / 2 / 1 slices per lane): each extra workgroup repeats a prologue of dependent loads that the
+  // 2-waves-per-SIMD kernel cannot hide.  Off by default; kept as a tested experiment path.
+  int bwd_regular_slices = 0;
+};
+Tuning& tuning();
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 inline bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
@@ -1238,7 +1348,7 @@ size_t lds_fwd(int cpb) {
 }
 template <int NT, int KMAX>
 size_t lds_fwd_regular(int cpb) {
-  return (size_t)cpb * NT * KMAX * sizeof(float2) + (size_t)NT * (KMAX / 4) * sizeof(unsigned) +
+  return (size_t)cpb * (NT * KMAX + 2) * sizeof(float2) + (size_t)NT * (KMAX / 4) * sizeof(unsigned) +
          (size_t)NT * KMAX * sizeof(int);
 }
 template <int NT>

@@ -1,0 +1,125 @@
+"""Kernel lab (not product code): launch-geometry sweeps of the aggregation kernels at the BASELINE
+config shapes, through the product entry points and ``mrp_tuning_set`` knobs, timed with HIP events
+over rotating buffer sets larger than 2x the 256 MB Infinity Cache (bench.py's method).
+
+Usage: python tools/sweep_geometry.py [fwd|bwd|all]
+"""
+import itertools
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import mrp_gnn_amd as mrp  # noqa: E402
+from bench import alg_bytes_bwd, alg_bytes_fwd, make_workload, rotating_sets, time_launches  # noqa: E402
+
+dev = torch.device("cuda:0")
+lib = mrp.load_library()
+MODE = mrp._lib.MODE_FILM_MEAN | mrp._lib.GB_LOGITS
+ITERS = int(os.environ.get("ITERS", "40"))
+
+SHAPES = {  # name: (B, N, C, H, knn)
+    "north_star": (32, 8, 512, 32, None),
+    "cfg1": (16, 8, 512, 32, None),
+    "cfg2": (32, 8, 1280, 8, None),
+    "cfg3": (8, 8, 2048, 8, None),
+    "cfg4": (8, 16, 1024, 16, 4),
+}
+
+
+def knobs(**kw):
+    lib.mrp_tuning_set(b"reset", 0)
+    for k, v in kw.items():
+        code = lib.mrp_tuning_set(k.encode(), int(v))
+        if code != 0:
+            raise ValueError(f"knob {k}={v} rejected")
+
+
+def setup(name):
+    B, N, C, H, knn = SHAPES[name]
+    g = make_workload(B, N, C, H, H, seed=1, device=dev, knn=knn)
+    torch.manual_seed(0)
+    gcn = mrp.GCN(type("O", (), {"feature_dim": C})()).to(dev)
+    with torch.no_grad():
+        z = gcn.edge_encoder.logits(g.edata["pose"])
+    return g, z, g.csr(dev)
+
+
+def fwd_time(g, z, csr):
+    x = g.ndata["image"]
+    Nt, C, H, W = x.shape
+    plane = x.numel() * 4
+    nf = rotating_sets(2 * plane)
+    sets = [(x if i == 0 else torch.randn_like(x), torch.empty_like(x)) for i in range(nf)]
+    launches = [lambda a=a, o=o: mrp.film_mean_forward_into(a, z, csr, MODE, o) for a, o in sets]
+    t = time_launches(launches, ITERS, dev)
+    return t, alg_bytes_fwd(Nt, g.num_edges(), C, H * W) / t / 8e12
+
+
+def bwd_time(g, z, csr):
+    x = g.ndata["image"]
+    Nt, C, H, W = x.shape
+    plane = x.numel() * 4
+    nb = rotating_sets(3 * plane)
+    sets = [(torch.randn_like(x), x if i == 0 else torch.randn_like(x)) for i in range(nb)]
+    launches = [lambda G=G, a=a: mrp.aggregate.film_mean_backward(G, a, z, csr, MODE, True, True) for G, a in sets]
+    t = time_launches(launches, ITERS, dev)
+    return t, alg_bytes_bwd(Nt, g.num_edges(), C, H * W) / t / 8e12
+
+
+def sweep(label, name, fn, grid):
+    g, z, csr = setup(name)
+    keys = list(grid)
+    res = []
+    for vals in itertools.product(*(grid[k] for k in keys)):
+        kw = dict(zip(keys, vals))
+        try:
+            knobs(**kw)
+            t, frac = fn(g, z, csr)
+        except (ValueError, RuntimeError) as e:
+            print(f"{label} {name} {kw}: {e}", flush=True)
+            continue
+        res.append((t, kw, frac))
+        print(f"{label} {name:10s} {kw}  {t * 1e6:8.1f} us  {frac * 100:5.1f} %", flush=True)
+    res.sort(key=lambda r: r[0])
+    print(f"BEST {label} {name}: {res[0][1]} {res[0][0] * 1e6:.1f} us {res[0][2] * 100:.1f} %", flush=True)
+    knobs()
+    del g, z, csr
+    torch.cuda.empty_cache()
+
+
+def main():
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    # warm the clocks
+    g, z, csr = setup("cfg2")
+    out = torch.empty_like(g.ndata["image"])
+    for _ in range(2000):
+        mrp.film_mean_forward_into(g.ndata["image"], z, csr, MODE, out)
+    torch.cuda.synchronize()
+    del g, z, csr, out
+    if what == "regbwd":
+        sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [1, 2], "bwd_regular_lanes": [8, 16, 32],
+                                        "bwd_regular_slices": [0, 1, 2, 4]})
+        for name in ("cfg2", "cfg3", "cfg1"):
+            sweep("bwd", name, bwd_time, {"bwd_fused_cap": [8]})
+            sweep("fwd", name, fwd_time, {"fwd_cap": [16]})
+        sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0, 1]})
+    if what in ("fwd", "all"):
+        for name in ("cfg2", "cfg3"):
+            sweep("fwd", name, fwd_time, {"fwd_lo": [4, 8, 16], "fwd_hi": [4, 8, 16], "fwd_cap": [4, 8, 16]})
+        sweep("fwd", "north_star", fwd_time, {"fwd_lo": [16, 32, 64], "fwd_hi": [32, 64, 128, 256], "fwd_cap": [8, 16]})
+        sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0, 1], "fwd_regular_lo": [8, 16, 32, 64],
+                                        "fwd_regular_hi": [16, 32, 64], "fwd_regular_cap": [4, 8, 16]})
+    if what in ("bwd", "all"):
+        for name in ("cfg2", "cfg3"):
+            sweep("bwd", name, bwd_time, {"bwd_fused_lo": [4, 8, 16], "bwd_fused_hi": [4, 8, 16],
+                                          "bwd_fused_cap": [8, 16, 32, 64]})
+        sweep("bwd", "cfg1", bwd_time, {"bwd_fused_lo": [32, 64], "bwd_fused_hi": [64, 128, 256],
+                                        "bwd_fused_cap": [2, 4, 8]})
+        sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [1, 2], "bwd_regular_lanes": [8, 16, 32],
+                                        "bwd_regular_slices": [0, 1, 2, 4]})
+
+
+if __name__ == "__main__":
+    main()
