@@ -218,6 +218,32 @@ int64_t mrp_film_mean_bwd_workspace(int32_t num_graphs, int32_t max_nodes, int32
                                     int32_t C, int32_t P);
 
 /*
+ * The layer's 1x1 compress convolution with the aggregation fused into it (dgl/model/models.py:181-184:
+ * g_h = gcn1(g); h = conv1(torch.cat((h, g_h), 1))), forward, fp32 on the matrix cores:
+ *
+ *   y[v, m, p] = sum_c W[m, c] x[v, c, p] + sum_c W[m, C + c] a[v, c, p] + bias[m]
+ *
+ * with a = the aggregate of mrp_film_mean_fwd (bit-identical), computed in the GEMM's operand
+ * producer: the (N, 2C, P) concatenation is never written.  wt is the conv weight (C, 2C, 1, 1)
+ * transposed to (2C, C) (k-major, 16-byte aligned); bias (C) may be NULL; y (num_nodes, C, P), node
+ * stride y_node_stride.  Supports graph_kind MRP_GRAPH_COMPLETE with 2..8 nodes per graph, P % 16 == 0
+ * and C % 128 == 0; returns hipErrorNotSupported otherwise (run mrp_film_mean_cat_fwd + a GEMM).
+ */
+int mrp_compress_film_fwd(const float* x, int64_t x_node_stride, const float* gb,
+                          int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
+                          int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode,
+                          const float* wt, const float* bias,
+                          float* y, int64_t y_node_stride, void* stream);
+
+/*
+ * gb[i] = sigmoid(z[i]) for n floats (n % 4 == 0, 16-byte aligned), the expression the aggregation
+ * kernels apply under MRP_AGG_GB_LOGITS, so a FiLM op fed gb without the flag gives the same bits as
+ * one fed z with it.  Replaces the Sigmoid of the edge encoder, dgl/model/models.py:149.  Used ahead
+ * of mrp_compress_film_fwd, whose workgroups would otherwise each re-evaluate the sigmoids.
+ */
+int mrp_film_gate(const float* z, float* gb, int64_t n, void* stream);
+
+/*
  * First layer of the edge encoder, dgl/model/models.py:147-148:  h = relu(pose W1^T + b1).
  *   pose (num_edges, 9), w1 (C, 9) (nn.Linear weight layout), b1 (C) -> h (num_edges, C), fp32.
  * The second Linear is a plain library GEMM and its Sigmoid is fused into the aggregation

@@ -25,6 +25,8 @@ EXPORTED_SYMBOLS = (
     "mrp_film_mean_fwd_ex",
     "mrp_film_mean_bwd_ex",
     "mrp_film_mean_bwd_workspace",
+    "mrp_compress_film_fwd",
+    "mrp_film_gate",
     "mrp_edge_hidden_fwd",
     "mrp_edge_encoder_bwd_workspace",
     "mrp_edge_encoder_bwd",
@@ -35,6 +37,8 @@ EXPORTED_SYMBOLS = (
 )
 ABI_VERSION = 10
 MAX_NODES = 16
+
+HIP_ERROR_NOT_SUPPORTED = 801  # hipErrorNotSupported: a fused path declines this shape
 
 MODE_FILM_MEAN = 0
 MODE_FILM_SUM = 1
@@ -86,6 +90,11 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_film_mean_bwd_workspace.restype = ctypes.c_int64
     lib.mrp_tuning_set.argtypes = [ctypes.c_char_p, _I32]
     lib.mrp_tuning_set.restype = ctypes.c_int
+    lib.mrp_compress_film_fwd.argtypes = [_P, _I64, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P,
+                                          _I64, _P]
+    lib.mrp_compress_film_fwd.restype = ctypes.c_int
+    lib.mrp_film_gate.argtypes = [_P, _P, _I64, _P]
+    lib.mrp_film_gate.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]

@@ -12,7 +12,11 @@ The module keeps the reference's ``nn.Conv2d`` parameters (``conv1.weight`` (C, 
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
+
+from . import _lib
 
 
 class Compress1x1Function(torch.autograd.Function):
@@ -53,3 +57,61 @@ def compress_1x1(conv: torch.nn.Conv2d, h: torch.Tensor) -> torch.Tensor:
             or conv.padding not in ((0, 0), "valid") or conv.dilation != (1, 1) or h.dtype != torch.float32:
         return conv(h)
     return Compress1x1Function.apply(h, conv.weight, conv.bias)
+
+
+def _weight_t(conv: torch.nn.Conv2d) -> torch.Tensor:
+    """The conv weight (C, 2C, 1, 1) transposed to (2C, C), k-major — the fused kernel's A operand
+    layout; cached on the module per weight version."""
+    w = conv.weight
+    key = (w.data_ptr(), w._version, w.device)
+    hit = getattr(conv, "_mrp_wt", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    wt = w.detach().reshape(w.shape[0], w.shape[1]).t().contiguous()
+    conv._mrp_wt = (key, wt)
+    return wt
+
+
+def compress_film_fused(conv: torch.nn.Conv2d, x: torch.Tensor, gb, csr, mode: int):
+    """``conv(torch.cat((x, film_mean(x, gb)), 1))`` (``models.py:181-184``) in ONE kernel
+    (``mrp_compress_film_fwd``): the aggregate is computed inside the 1x1 GEMM's operand producer and
+    the (N, 2C, H, W) concatenation never reaches HBM.  Forward only (no autograd).  Returns None
+    when the kernel does not cover the shape (non-complete graphs, N > 8, P % 16, C % 128): the
+    caller then runs the cat kernel + batched GEMM."""
+    n, C, H, W = x.shape
+    if (not x.is_cuda or x.dtype != torch.float32 or conv.kernel_size != (1, 1) or conv.groups != 1
+            or conv.stride != (1, 1) or conv.dilation != (1, 1) or conv.padding not in ((0, 0), "valid")
+            or tuple(conv.weight.shape[:2]) != (C, 2 * C) or conv.weight.dtype != torch.float32):
+        return None
+    if csr.graph_kind != _lib.GRAPH_COMPLETE or not 2 <= csr.max_nodes <= 8 or (H * W) % 16 or C % 128:
+        return None
+    from .aggregate import _ptr, _stream, node_stride
+    xs = node_stride(x)
+    if xs is None:
+        x = x.contiguous()
+        xs = C * H * W
+    lib = _lib.load_library()
+    if gb is not None:
+        gb = gb.reshape(csr.num_edges, C, 2)
+        if not gb.is_contiguous() or gb.dtype != torch.float32:
+            gb = gb.contiguous().float()
+        if mode & _lib.GB_LOGITS:
+            # one elementwise pass to post-sigmoid pairs (the kernels' own sigmoid: same bits as the
+            # logits path) instead of 2 x E x C sigmoids in every workgroup of a channel column
+            gate = torch.empty_like(gb)
+            with torch.cuda.device(x.device):
+                _lib.check(lib.mrp_film_gate(_ptr(gb), _ptr(gate), gb.numel(), _stream(x.device)), "mrp_film_gate")
+            gb, mode = gate, mode & ~_lib.GB_LOGITS
+    wt = _weight_t(conv)
+    bias = conv.bias.detach() if conv.bias is not None else None
+    if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
+        bias = bias.float().contiguous()
+    y = torch.empty((n, C, H, W), device=x.device, dtype=torch.float32)
+    with torch.cuda.device(x.device):
+        code = lib.mrp_compress_film_fwd(_ptr(x), xs, _ptr(gb), csr.num_graphs, csr.max_nodes, csr.graph_kind,
+                                         csr.num_nodes, csr.num_edges, C, H * W, mode, _ptr(wt), _ptr(bias),
+                                         _ptr(y), C * H * W, _stream(x.device))
+    if code == _lib.HIP_ERROR_NOT_SUPPORTED:
+        return None
+    _lib.check(code, "mrp_compress_film_fwd")
+    return y

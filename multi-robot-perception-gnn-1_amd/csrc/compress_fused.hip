@@ -1,0 +1,469 @@
+// compress_fused.hip — the GCN layer's 1x1 compress convolution with the FiLM-mean aggregation
+// fused into its operand producer, on the fp32 matrix cores of gfx950 (MI355X / CDNA4).
+//
+// Reference (xjh19971/multi-robot-perception-gnn-1, dgl/model/models.py:181-184):
+//     g_h = self.gcn1(g)                       # update_all(edge_udf, node_udf), :207-211,223
+//     h   = torch.cat((h, g_h), dim=1)          # (Nt, 2C, H, W)
+//     h   = self.conv1(h)                       # nn.Conv2d(2C, C, 1): Y = W [x; agg] + b
+// Here, per destination node v and pixel p:
+//     Y[v, m, p] = sum_c W[m, c] x[v, c, p] + sum_c W[m, C + c] agg[v, c, p] + b[m]
+// without the (Nt, 2C, P) concatenation buffer ever reaching HBM: each workgroup loads the slices of
+// x of all nodes of ONE graph for a 16-pixel tile and a 16-channel stage, computes the aggregate of
+// every node from those same registers (the reference's rounding: fl(fl(gamma x) + beta), sequential
+// sum over in-edges by ascending source, true division), and feeds both halves to
+// v_mfma_f32_16x16x4_f32 (f32 in, f32 accumulate: exact fp32 products, an fmaf chain per output).
+//
+// Work decomposition: workgroup = (graph b, 16-pixel tile, 128 output channels); 8 waves: 4 consumer
+// waves (MFMA only) and 4 producer waves (loads, aggregate, LDS stores) — see the kernel.  The K loop
+// runs over stages of 16 input channels: per stage every consumer wave issues 4 k-steps x 2 halves x
+// 2 x N MFMAs (128 at N = 8) while the producers fill the other buffer with stage s+1.
+//
+// Supported: complete graphs (the reference topology, arithmetic edge ids) of N <= 8 nodes,
+// P % 16 == 0, C % 128 == 0, mean/sum FiLM modes (gamma/beta as logits or post-sigmoid).  Anything
+// else returns hipErrorNotSupported and the caller runs the unfused kernels (cat + library GEMM).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mrp_gnn.h"
+
+namespace mrp_cf {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kProducers = 4;  // load / aggregate / LDS-store waves
+constexpr int TP = 16;         // pixels per workgroup
+constexpr int KS = 16;         // input channels per stage (4 per producer wave)
+
+// NC consumer (MFMA) waves, 32 output channels each: BM = 32 NC output channels per workgroup
+template <int NC>
+struct Geo {
+  static constexpr int BM = 32 * NC;
+  static constexpr int WROW = BM + 16;                 // W stage row, padded: k rows 16 banks apart
+  static constexpr int THREADS = 64 * (NC + kProducers);
+  static constexpr int WF4 = 2 * KS * BM / 4 / (64 * kProducers);  // W float4 per producer lane per stage
+};
+
+struct Args {
+  const float* x;
+  int64_t xs;
+  const float* gb;  // (E, C, 2)
+  const float* wt;  // (2C, C): conv weight transposed, k-major
+  const float* bias;
+  float* y;
+  int64_t ys;
+  int32_t C, P, ntiles_p, ntiles_m, mode, logits, remap;
+  int32_t debug;  // kernel lab only: 1 = producers skip their work, 2 = consumers skip the MFMAs,
+                  // 32 = no producer priority, 64 = BM 128 even where C allows 256
+};
+
+__device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
+
+// x / D correctly rounded (== the IEEE division the oracle and the other kernels use) in three
+// instructions: q0 = x * RN(1/D), r = fma(-q0, D, x) (exact), q = fma(r, RN(1/D), q0).  Checked
+// exhaustively over all 2^32 fp32 x for D = 2..15 (tools/check_div_const.c): equal except for
+// |x| < 2^-124, +-0 and +-inf, which take the IEEE division.
+// The caller checks the range once for a whole set of quotients (div_fast_ok) and redoes the set
+// with the IEEE division when any lane is out of it, so the fast path has no branch per quotient.
+template <int D>
+__device__ __forceinline__ float div_fast(float x) {
+  constexpr float y = 1.0f / (float)D;
+  const float q0 = __fmul_rn(x, y);
+  const float r = __builtin_fmaf(-q0, (float)D, x);
+  return __builtin_fmaf(r, y, q0);
+}
+// min |x| >= 2^-124 and max |x| < inf (NaN inputs give NaN either way)
+__device__ __forceinline__ bool div_fast_ok(float mn, float mx) { return mn >= 0x1p-124f && mx < __builtin_inff(); }
+
+__device__ __forceinline__ const float* at_bytes(const float* base, uint32_t off) {
+  return reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + off);
+}
+
+// DPP row_newbcast: every lane of a 16-lane row gets lane src's value of that row.  src must fold to a
+// constant after unrolling (the DPP control is an immediate); the switch then folds away.  With full
+// row/bank masks and bound_ctrl the compiler folds the move into the consuming v_mul / v_add (_dpp).
+__device__ __forceinline__ float row_bcast(float v, int src) {
+  const int i = __builtin_bit_cast(int, v);
+  int r;
+  switch (src) {
+#define MRP_CF_BCAST(n) \
+  case n: r = __builtin_amdgcn_update_dpp(0, i, 0x150 + n, 0xf, 0xf, true); break;
+    MRP_CF_BCAST(0) MRP_CF_BCAST(1) MRP_CF_BCAST(2) MRP_CF_BCAST(3) MRP_CF_BCAST(4) MRP_CF_BCAST(5)
+    MRP_CF_BCAST(6) MRP_CF_BCAST(7) MRP_CF_BCAST(8) MRP_CF_BCAST(9) MRP_CF_BCAST(10) MRP_CF_BCAST(11)
+    MRP_CF_BCAST(12) MRP_CF_BCAST(13) MRP_CF_BCAST(14) default: r = __builtin_amdgcn_update_dpp(0, i, 0x15f, 0xf, 0xf, true);
+#undef MRP_CF_BCAST
+  }
+  return __builtin_bit_cast(float, r);
+}
+
+template <int NT, int NC>
+struct Lds {
+  static constexpr int XS = NT * KS * TP;        // x stage  [node][ch][pix]
+  static constexpr int WS = 2 * KS * Geo<NC>::WROW;  // W stage  [half][k][m]
+  static constexpr int BUF = 2 * XS + WS;        // x, aggregate, W
+  static constexpr int TOTAL = 2 * BUF;          // double buffer
+};
+
+// Roles (wave-uniform): waves 0..NC-1 are consumers — each owns output rows [32w, 32w + 32) x all N
+// nodes x 16 pixels (2 x N accumulator blocks) and only reads LDS and issues MFMAs; the last 4 waves
+// are producers — producer p fills channels [4p, 4p + 4) of the next stage: x slices of all N nodes,
+// gamma/beta in registers (one edge per lane and slot), the aggregate from the same registers, and a
+// quarter of the W stage.  Consumer and producer waves share each SIMD: the MFMA pipe and the
+// VALU/memory work of the producer run concurrently (MI355X_MICROARCH.md, wave scheduling).  One
+// workgroup barrier per stage hands the double-buffered stage over.  The aggregate of a (graph, pixel
+// tile, stage) is recomputed by each of the C / BM workgroups of its output-channel column, so the
+// wider tile (NC = 8, BM = 256) halves the producers' work per MFMA.
+template <int NT, int NC, bool FILM, bool LOGITS, bool MEAN>
+__global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
+  using L = Lds<NT, NC>;
+  constexpr int BM = Geo<NC>::BM, WROW = Geo<NC>::WROW, WF4 = Geo<NC>::WF4;
+  extern __shared__ f4 smem_f4[];
+  float* smem = reinterpret_cast<float*>(smem_f4);
+
+  // block -> (graph, pixel tile, m tile); with remap, the m tiles of one (graph, pixel tile) are dealt
+  // to the same XCD (blocks i and i + 8 share one), so their shared x slices hit that XCD's L2
+  int id = blockIdx.x;
+  if (a.remap) id = (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+  const int mt = id % a.ntiles_m;
+  const int rest = id / a.ntiles_m;
+  const int pt = rest % a.ntiles_p;
+  const int b = rest / a.ntiles_p;
+  const int m0 = mt * BM, p0 = pt * TP;
+  const int node0 = b * NT;
+  const int64_t ebase = (int64_t)b * NT * (NT - 1);
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nstages = a.C / KS;
+
+  if (w >= NC) {
+    // ------------------------------------------------------------------ producer
+    // the producers' VALU would otherwise lose issue arbitration to the (older) consumer waves and
+    // finish only after the consumers wait at the barrier (MI355X_MICROARCH.md, two waves per SIMD):
+    // at high priority it fills the issue slots an MFMA leaves free (8 of its 32 cycles are held)
+    if (!(a.debug & 32)) __builtin_amdgcn_s_setprio(2);
+    const int pw = w - NC;                    // 0..3
+    const int pt_id = pw * 64 + lane;         // 0..255 within the producers
+    const int cl = lane >> 4, px = lane & 15;  // (channel within the wave's 4, pixel): one 16-lane DPP row per channel
+    const int pch = 4 * pw + cl;              // channel within the stage
+    constexpr int NE = NT * (NT - 1);          // edges of a graph
+    constexpr int GI = (NE + 15) / 16;         // gamma/beta pairs per lane: lane px of a row holds edges px + 16 i
+    // x (from HBM) is loaded two stages before it is stored to LDS, in two alternating register sets;
+    // W and gamma/beta (L2-resident) one stage before, in one set — two sets of everything spilled at
+    // BM = 256.  Issue order per stage: W + gamma/beta of the next stage, then x of the one after, so
+    // waiting for the next stage's operands leaves the newest x loads in flight.
+    struct XRegs {
+      float xr[NT];
+    };
+    struct WRegs {
+      f4 wr[WF4];
+      float2 gr[GI];
+    };
+    XRegs X0, X1;
+    WRegs WG;
+    const int last = nstages - 1;
+    // addressing: buffer loads — a wave-uniform resource per operand (x of this graph and pixel tile,
+    // W of this m tile, gamma/beta of this graph), a per-lane 32-bit voffset fixed for the whole loop
+    // and a wave-uniform soffset per stage (SGPR).  With flat pointers the compiler re-associated the
+    // uniform and per-lane parts into 64-bit per-lane pointers (VGPR pairs + 64-bit adds per stage).
+    // The host guarantees every byte offset fits in 31 bits.
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.x + (int64_t)node0 * a.xs + p0), 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.wt + m0), 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.gb != nullptr ? a.gb + ebase * a.C * 2 : a.x), 0, 0x7fffffff, 0x00020000);
+    const uint32_t x_off = (uint32_t)(pch * a.P + px) * 4u;
+    uint32_t w_off[WF4];
+#pragma unroll
+    for (int i = 0; i < WF4; ++i) {
+      const int idx = pt_id + i * 256;
+      const int m4 = idx % (BM / 4), k = (idx / (BM / 4)) % KS, h = idx / (BM / 4 * KS);
+      w_off[i] = (uint32_t)((h * a.C + k) * a.C + 4 * m4) * 4u;
+    }
+    uint32_t g_off[GI];
+#pragma unroll
+    for (int i = 0; i < GI; ++i) g_off[i] = (uint32_t)((min(px + 16 * i, NE - 1) * a.C + pch) * 2) * 4u;
+    auto issue_x = [&](XRegs& R, int s) {
+      const int c0 = s * KS;
+#pragma unroll
+      for (int u = 0; u < NT; ++u)
+        R.xr[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, x_off, (c0 * a.P + u * (int)a.xs) * 4, 0));
+    };
+    auto issue_wg = [&](WRegs& R, int s) {
+      const int c0 = s * KS;
+#pragma unroll
+      for (int i = 0; i < WF4; ++i)  // W stage: 2 halves x 16 k x BM m
+        R.wr[i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wr, w_off[i], c0 * a.C * 4, 0));
+      // slots past the graph's NE edges reload the last edge (never read): no divergent branch around
+      // the loads, so the compiler counts them exactly
+#pragma unroll
+      for (int i = 0; i < GI; ++i) {
+        if (FILM) {
+          R.gr[i] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(gr, g_off[i], c0 * 2 * 4, 0));
+        }
+      }
+    };
+    auto produce = [&](const XRegs& X, const WRegs& R, int buf) {
+      float* Xs = smem + buf * L::BUF;
+      float* As = Xs + L::XS;
+      float* Ws = As + L::XS;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) Xs[(u * KS + pch) * TP + px] = X.xr[u];
+#pragma unroll
+      for (int i = 0; i < WF4; ++i) {
+        const int idx = pt_id + i * 256;
+        const int m4 = idx % (BM / 4), k = (idx / (BM / 4)) % KS, h = idx / (BM / 4 * KS);
+        *reinterpret_cast<f4*>(Ws + (h * KS + k) * WROW + 4 * m4) = R.wr[i];
+      }
+      float gam[GI], bet[GI];
+#pragma unroll
+      for (int i = 0; i < GI; ++i) {
+        gam[i] = LOGITS ? sigmoidf(R.gr[i].x) : R.gr[i].x;
+        bet[i] = LOGITS ? sigmoidf(R.gr[i].y) : R.gr[i].y;
+      }
+      // agg[v] = sum over u != v, ascending, of fl(fl(gamma_uv x_u) + beta_uv): gamma/beta of edge
+      // e = u -> v (i-major ids, dgl/dataloader.py:88-95) sit in lane e % 16 of this channel's row,
+      // slot e / 16, and reach every pixel lane by a DPP row broadcast (no LDS round trip)
+      float sum[NT];
+      float mn = __builtin_inff(), mx = 0.f;
+#pragma unroll
+      for (int v = 0; v < NT; ++v) {
+        // all products, then all + beta, then the sum: a DPP instruction reading a VGPR written by
+        // the previous VALU instruction needs two wait states (s_nop), so no DPP op consumes the
+        // result right before it
+        float m[NT];
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          if (u == v) continue;
+          m[u] = X.xr[u];
+          if (FILM) {
+            const int e = u * (NT - 1) + (v < u ? v : v - 1);
+            m[u] = __fmul_rn(row_bcast(gam[e >> 4], e & 15), m[u]);
+          }
+        }
+        if (FILM) {
+#pragma unroll
+          for (int u = 0; u < NT; ++u) {
+            if (u == v) continue;
+            const int e = u * (NT - 1) + (v < u ? v : v - 1);
+            m[u] = __fadd_rn(row_bcast(bet[e >> 4], e & 15), m[u]);
+          }
+        }
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          if (u == v) continue;
+          acc = __fadd_rn(acc, m[u]);
+        }
+        sum[v] = acc;
+        if (MEAN && NT > 2) {
+          mn = fminf(mn, __builtin_fabsf(acc));
+          mx = fmaxf(mx, __builtin_fabsf(acc));
+        }
+      }
+      if (MEAN && NT > 2) {
+        if (__builtin_expect(!div_fast_ok(mn, mx), 0)) {
+#pragma unroll
+          for (int v = 0; v < NT; ++v) sum[v] = sum[v] / (float)(NT - 1);
+        } else {
+#pragma unroll
+          for (int v = 0; v < NT; ++v) sum[v] = div_fast<NT - 1>(sum[v]);
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < NT; ++v) As[(v * KS + pch) * TP + px] = sum[v];
+    };
+    // stage t: x in register set t & 1, LDS buffer t & 1.  nstages is a multiple of 8 (C % 128 == 0).
+    // The loop body has no conditional loads (stage indices are clamped instead): with a path that
+    // skipped them the compiler's wait counts would merge to "everything", draining the loads in
+    // flight.
+    issue_x(X0, 0);
+    issue_wg(WG, 0);
+    issue_x(X1, 1);
+    produce(X0, WG, 0);
+    issue_wg(WG, 1);
+    issue_x(X0, min(2, last));
+    if (a.debug & 1) {  // lab: consumers only
+      for (int s = 0; s < nstages; ++s) __syncthreads();
+      return;
+    }
+    for (int s = 0; s < nstages - 2; s += 2) {
+      __syncthreads();  // barrier #s: stage s complete in LDS, stage s-1 consumed
+      produce(X1, WG, 1);  // stage s+1
+      issue_wg(WG, s + 2);
+      issue_x(X1, s + 3);
+      __syncthreads();  // barrier #(s+1)
+      produce(X0, WG, 0);  // stage s+2
+      issue_wg(WG, min(s + 3, last));
+      issue_x(X0, min(s + 4, last));
+    }
+    __syncthreads();  // barrier #(nstages-2)
+    produce(X1, WG, 1);  // the last stage
+    __syncthreads();  // barrier #(nstages-1)
+    return;
+  }
+
+  // -------------------------------------------------------------------- consumer
+  f32x4 acc[2][NT];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[mb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int lk = lane >> 4, lc = lane & 15;
+  for (int s = 0; s < nstages; ++s) {
+    __syncthreads();  // stage s is in LDS; the producers now fill stage s+1 in the other buffer
+    const float* Xs = smem + (s & 1) * L::BUF;
+    const float* As = Xs + L::XS;
+    const float* Ws = As + L::XS;
+    if (a.debug & 2) continue;  // lab: producers only
+#pragma unroll
+    for (int k4 = 0; k4 < KS / 4; ++k4) {
+      const int k = 4 * k4 + lk;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float* Bsrc = h == 0 ? Xs : As;
+        float af[2];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) af[mb] = Ws[(h * KS + k) * WROW + 32 * w + 16 * mb + lc];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const float bf = Bsrc[(j * KS + k) * TP + lc];
+#pragma unroll
+          for (int mb = 0; mb < 2; ++mb) acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mb], bf, acc[mb][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // epilogue: D[row = 4 (lane >> 4) + r][col = lane & 15] of block (mb, node j), + bias
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + 32 * w + 16 * mb + 4 * lk + r;
+      const float bm = a.bias != nullptr ? a.bias[m] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        float* yp = a.y + (int64_t)(node0 + j) * a.ys + (int64_t)m * a.P + p0 + lc;
+        __builtin_nontemporal_store(__fadd_rn(acc[mb][j][r], bm), yp);
+      }
+    }
+  }
+}
+
+// gamma/beta = sigmoid(z), the aggregation kernels' own expression (film_mean_kernels.hpp sigmoidf):
+// the fused kernel then reads post-sigmoid pairs instead of evaluating 2 x NE sigmoids per channel in
+// every workgroup of a (graph, channel) column
+__global__ void __launch_bounds__(256) film_gate(const float4* __restrict__ z, float4* __restrict__ g, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = z[i];
+    g[i] = make_float4(sigmoidf(v.x), sigmoidf(v.y), sigmoidf(v.z), sigmoidf(v.w));
+  }
+}
+
+}  // namespace mrp_cf
+
+namespace {
+
+int mrp_cf_debug = 0;
+
+template <int NT, int NC, bool FILM, bool LOGITS, bool MEAN>
+hipError_t launch_mode(const mrp_cf::Args& a, int64_t grid, hipStream_t st) {
+  const size_t lds = (size_t)mrp_cf::Lds<NT, NC>::TOTAL * sizeof(float);  // N = 8: 68 KB (NC 4), 101 KB (NC 8)
+  auto* kern = &mrp_cf::compress_film_fwd<NT, NC, FILM, LOGITS, MEAN>;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(mrp_cf::Geo<NC>::THREADS), lds, st, a);
+  return hipGetLastError();
+}
+
+// the FiLM mode is a template parameter: evaluated per edge term at run time it left the producers'
+// inner loops full of branches
+template <int NT, int NC>
+hipError_t launch_nc(const mrp_cf::Args& a, int64_t grid, hipStream_t st) {
+  if (a.mode == MRP_AGG_COPY_MEAN) return launch_mode<NT, NC, false, false, true>(a, grid, st);
+  const bool mean = a.mode == MRP_AGG_FILM_MEAN;
+  if (a.logits)
+    return mean ? launch_mode<NT, NC, true, true, true>(a, grid, st) : launch_mode<NT, NC, true, true, false>(a, grid, st);
+  return mean ? launch_mode<NT, NC, true, false, true>(a, grid, st) : launch_mode<NT, NC, true, false, false>(a, grid, st);
+}
+
+// BM = 256 output channels per workgroup when C allows it (and the lab hook does not force 128)
+template <int NT>
+hipError_t launch(mrp_cf::Args a, int32_t num_graphs, hipStream_t st) {
+  const int nc = (a.C % 256 == 0 && !(a.debug & 64)) ? 8 : 4;
+  a.ntiles_m = a.C / (32 * nc);
+  const int64_t grid = (int64_t)num_graphs * a.ntiles_p * a.ntiles_m;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  a.remap = grid % 8 == 0 ? 1 : 0;
+  return nc == 8 ? launch_nc<NT, 8>(a, grid, st) : launch_nc<NT, 4>(a, grid, st);
+}
+
+}  // namespace
+
+extern "C" int mrp_film_gate(const float* z, float* gb, int64_t n, void* stream) {
+  if (n < 0 || n % 4 != 0) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  if (z == nullptr || gb == nullptr || (reinterpret_cast<uintptr_t>(z) & 15) || (reinterpret_cast<uintptr_t>(gb) & 15))
+    return hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  const int64_t blocks = (n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096;
+  hipLaunchKernelGGL(mrp_cf::film_gate, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     reinterpret_cast<const float4*>(z), reinterpret_cast<float4*>(gb), n4);
+  return hipGetLastError();
+}
+
+// kernel-lab hook (tools/exp_compress_fused.py): not part of the ABI header
+extern "C" void mrp_compress_film_debug(int mode) { mrp_cf_debug = mode; }
+
+extern "C" int mrp_compress_film_fwd(const float* x, int64_t x_node_stride, const float* gb, int32_t num_graphs,
+                                     int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges,
+                                     int32_t C, int32_t P, int32_t mode_flags, const float* wt, const float* bias,
+                                     float* y, int64_t y_node_stride, void* stream) {
+  const int32_t logits = (mode_flags & MRP_AGG_GB_LOGITS) ? 1 : 0;
+  const int32_t mode = mode_flags & ~MRP_AGG_GB_LOGITS;
+  if (num_graphs < 0 || C < 0 || P < 0 || mode < MRP_AGG_FILM_MEAN || mode > MRP_AGG_COPY_MEAN)
+    return hipErrorInvalidValue;
+  if (graph_kind != MRP_GRAPH_COMPLETE || max_nodes < 2 || max_nodes > 8 || P % mrp_cf::TP != 0 ||
+      C % 128 != 0 || C == 0)
+    return hipErrorNotSupported;
+  if ((int64_t)num_graphs * max_nodes != num_nodes ||
+      (int64_t)num_graphs * max_nodes * (max_nodes - 1) != num_edges)
+    return hipErrorInvalidValue;
+  if (num_graphs == 0 || P == 0) return hipSuccess;
+  const int64_t plane = (int64_t)C * P;
+  if (x == nullptr || y == nullptr || wt == nullptr || x_node_stride < plane || y_node_stride < plane)
+    return hipErrorInvalidValue;
+  if (mode != MRP_AGG_COPY_MEAN && gb == nullptr) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(wt) & 15) != 0) return hipErrorInvalidValue;  // float4 W loads
+  // buffer-load byte offsets are 31-bit: x of one graph, the (2C, C) weight
+  if ((int64_t)(max_nodes - 1) * x_node_stride * 4 + plane * 4 >= (1LL << 31) || (int64_t)2 * C * C * 4 >= (1LL << 31))
+    return hipErrorNotSupported;
+  mrp_cf::Args a;
+  a.x = x;
+  a.xs = x_node_stride;
+  a.gb = gb;
+  a.wt = wt;
+  a.bias = bias;
+  a.y = y;
+  a.ys = y_node_stride;
+  a.C = C;
+  a.P = P;
+  a.ntiles_p = P / mrp_cf::TP;
+  a.mode = mode;
+  a.logits = logits;
+  a.debug = mrp_cf_debug;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  switch (max_nodes) {
+    case 2: return launch<2>(a, num_graphs, st);
+    case 3: return launch<3>(a, num_graphs, st);
+    case 4: return launch<4>(a, num_graphs, st);
+    case 5: return launch<5>(a, num_graphs, st);
+    case 6: return launch<6>(a, num_graphs, st);
+    case 7: return launch<7>(a, num_graphs, st);
+    case 8: return launch<8>(a, num_graphs, st);
+    default: return hipErrorNotSupported;
+  }
+}

@@ -34,7 +34,7 @@ import torch
 import torch.nn as nn
 
 from .aggregate import film_mean, film_mean_cat, film_mean_mix, film_mean_residual
-from .compress import compress_1x1
+from .compress import compress_1x1, compress_film_fused
 from .encoder import edge_logits
 
 
@@ -129,6 +129,22 @@ class GCN(nn.Module):
         return film_mean_cat(x, z, g.csr(x.device), mode, logits=True)
 
 
+    def forward_cat_compress(self, g, feats: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+        """``conv(torch.cat((feats, self(g, feats)), 1))`` (``models.py:181-184``).  Without autograd
+        (eval, ``test_dgl``) the aggregation runs inside the compress GEMM's operand producer
+        (``mrp_compress_film_fwd``: one kernel, no concatenation buffer) where that kernel covers the
+        shape; otherwise the cat kernel + batched GEMM."""
+        x = feats
+        if (x.is_cuda and self._return_mode() != "input" and not torch.is_grad_enabled()
+                and _opt(self.opt, "gcn_mode", "film_mean") != "copy_mean"
+                and fused_compress_enabled(x.shape[-2] * x.shape[-1])):
+            mode = _lib_modes()[_opt(self.opt, "gcn_mode", "film_mean")]
+            z = self.edge_encoder.logits(g.edata["pose"])
+            y = compress_film_fused(conv, x, z, g.csr(x.device), mode | _lib_logits())
+            if y is not None:
+                return y
+        return compress_1x1(conv, self.forward_cat(g, x))
+
     def forward_residual(self, g, feats: torch.Tensor = None) -> torch.Tensor:
         """``feats + self(g, feats)`` in one kernel pass: the residual combination ``h = g_h + h``
         of ``dgl/model/dgl_models.py:36-37`` (the FiLM-mean 'add' variant)."""
@@ -152,6 +168,40 @@ class GCN(nn.Module):
             return film_mean_mix(x, None, g.csr(x.device), x0, alpha, mode)
         z = self.edge_encoder.logits(g.edata["pose"])
         return film_mean_mix(x, z, g.csr(x.device), x0, alpha, mode, logits=True)
+
+
+_FUSED_COMPRESS = ["auto"]
+# "auto": the fused kernel where it measured faster than cat kernel + library GEMM (DESIGN.md,
+# fused compress): large planes (configs[1], 32x32: 1.18 ms vs 1.25 ms per layer); on 8x8 planes
+# (configs[2]/[3]) the 4 pixel tiles per graph leave the grid short and the unfused path wins
+FUSED_MIN_PLANE = 256
+
+
+def fused_compress_enabled(plane: int = None) -> bool:
+    v = _FUSED_COMPRESS[0]
+    if v == "auto":
+        return plane is not None and plane >= FUSED_MIN_PLANE
+    return bool(v)
+
+
+def fused_compress_setting():
+    return _FUSED_COMPRESS[0]
+
+
+def set_fused_compress(enabled) -> None:
+    """The fused aggregation + compress kernel (inference path): True (wherever the kernel covers the
+    shape), False (never) or "auto" (default: where it measured faster)."""
+    _FUSED_COMPRESS[0] = "auto" if enabled == "auto" else bool(enabled)
+
+
+def _lib_modes():
+    from . import _lib
+    return _lib.MODES
+
+
+def _lib_logits():
+    from . import _lib
+    return _lib.GB_LOGITS
 
 
 #: layer compositions of a GCN stack (``GCNStack``, ``multi_view_dgl_model``)
@@ -197,10 +247,10 @@ def _run_stack(module: nn.Module, g, h: torch.Tensor) -> torch.Tensor:
     alpha = float(_opt(module.opt, "gcn2_alpha", 0.1))
     for i in range(1, module.gcn_layers + 1):
         gcn = getattr(module, f"gcn{i}")
-        if module.gcn_combine in ("cat_compress", "cat"):
+        if module.gcn_combine == "cat_compress":
+            h = gcn.forward_cat_compress(g, h, getattr(module, f"conv{i}"))  # conv_i(cat((h, gcn_i(h)), 1))
+        elif module.gcn_combine == "cat":
             h = gcn.forward_cat(g, h)  # cat((h, gcn_i(h)), 1), one kernel pass
-            if module.gcn_combine == "cat_compress":
-                h = compress_1x1(getattr(module, f"conv{i}"), h)
         elif module.gcn_combine == "residual":
             h = gcn.forward_residual(g, h)
         else:
