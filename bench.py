@@ -305,6 +305,20 @@ def config_record(cid, world, rank, device, args):
         t = timed(fwd, args.config_steps, world, device, args.dist_backend)
     rec["forward"] = {"value": world * elems / t if scaling == "weak" else None, "unit": "elems/s",
                       "ms_per_step": t * 1e3}
+    # which compress path the eval forward took, and the other one for comparison (models.py policy)
+    fused = (mrp.models.fused_compress_enabled(P)
+             and mrp.compress.fused_compress_supported(net.conv1, x, csr))
+    prev = mrp.models.fused_compress_setting()
+    mrp.models.set_fused_compress(not fused)
+    try:
+        with torch.no_grad():
+            for _ in range(2):
+                fwd()
+            t_other = timed(fwd, args.config_steps, world, device, args.dist_backend)
+    finally:
+        mrp.models.set_fused_compress(prev)
+    rec["forward"]["compress"] = "fused aggregation + MFMA compress kernel" if fused else "cat kernel + library GEMM"
+    rec["forward"]["ms_per_step_other_compress"] = t_other * 1e3
     if scaling == "strong":  # every rank holds a different part of one global batch
         tot = torch.tensor([float(elems)], dtype=torch.float64,
                            device=device if args.dist_backend == "nccl" else "cpu")

@@ -224,11 +224,20 @@ int64_t mrp_film_mean_bwd_workspace(int32_t num_graphs, int32_t max_nodes, int32
  *   y[v, m, p] = sum_c W[m, c] x[v, c, p] + sum_c W[m, C + c] a[v, c, p] + bias[m]
  *
  * with a = the aggregate of mrp_film_mean_fwd (bit-identical), computed in the GEMM's operand
- * producer: the (N, 2C, P) concatenation is never written.  wt is the conv weight (C, 2C, 1, 1)
- * transposed to (2C, C) (k-major, 16-byte aligned); bias (C) may be NULL; y (num_nodes, C, P), node
- * stride y_node_stride.  Supports graph_kind MRP_GRAPH_COMPLETE with 2..8 nodes per graph, P % 16 == 0
- * and C % 128 == 0; returns hipErrorNotSupported otherwise (run mrp_film_mean_cat_fwd + a GEMM).
+ * producer: the (N, 2C, P) concatenation is never written.  wt is the conv weight packed by
+ * mrp_compress_weight_pack (2C^2 floats, 16-byte aligned); bias (C) may be NULL; y (num_nodes, C, P),
+ * node stride y_node_stride.  Supports graph_kind MRP_GRAPH_COMPLETE with 2..8 nodes per graph,
+ * P % 16 == 0, C % 128 == 0, (max_nodes - 1) x_node_stride + C P < 2^29 and C < 16384 (31-bit buffer
+ * offsets); returns hipErrorNotSupported otherwise (run mrp_film_mean_cat_fwd + a GEMM).
  */
+/*
+ * Packs the 1x1 compress weight w (C, 2C) (nn.Conv2d(2C, C, 1).weight, row-major) into the layout
+ * mrp_compress_film_fwd reads: wp[h][s][lk][m][k4] = w[m][h C + 16 s + 4 k4 + lk] (h < 2, s < C/16,
+ * lk < 4, m < C, k4 < 4) — each 16-byte group is one MFMA lane's four k-steps of a 16-channel stage.
+ * C % 16 == 0; wp 16-byte aligned, 2C^2 floats.  Run once per weight update.
+ */
+int mrp_compress_weight_pack(const float* w, float* wp, int32_t C, void* stream);
+
 int mrp_compress_film_fwd(const float* x, int64_t x_node_stride, const float* gb,
                           int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
                           int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode,

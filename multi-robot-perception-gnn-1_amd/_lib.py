@@ -15,7 +15,8 @@ import threading
 import torch  # noqa: F401  (must be loaded before the HIP library, see module docstring)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
+# MRP_GNN_LIB: kernel-lab A/B of an alternative in-tree build (tools/); the product loads lib/libmrp_gnn.so
+LIB_PATH = os.environ.get("MRP_GNN_LIB") or os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
 
 #: Every symbol ``include/mrp_gnn.h`` declares.
 EXPORTED_SYMBOLS = (
@@ -27,6 +28,7 @@ EXPORTED_SYMBOLS = (
     "mrp_film_mean_bwd_workspace",
     "mrp_compress_film_fwd",
     "mrp_film_gate",
+    "mrp_compress_weight_pack",
     "mrp_edge_hidden_fwd",
     "mrp_edge_encoder_bwd_workspace",
     "mrp_edge_encoder_bwd",
@@ -95,6 +97,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_compress_film_fwd.restype = ctypes.c_int
     lib.mrp_film_gate.argtypes = [_P, _P, _I64, _P]
     lib.mrp_film_gate.restype = ctypes.c_int
+    lib.mrp_compress_weight_pack.argtypes = [_P, _P, _I32, _P]
+    lib.mrp_compress_weight_pack.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]

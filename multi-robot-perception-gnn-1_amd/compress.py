@@ -59,17 +59,36 @@ def compress_1x1(conv: torch.nn.Conv2d, h: torch.Tensor) -> torch.Tensor:
     return Compress1x1Function.apply(h, conv.weight, conv.bias)
 
 
-def _weight_t(conv: torch.nn.Conv2d) -> torch.Tensor:
-    """The conv weight (C, 2C, 1, 1) transposed to (2C, C), k-major — the fused kernel's A operand
-    layout; cached on the module per weight version."""
+def _weight_packed(conv: torch.nn.Conv2d) -> torch.Tensor:
+    """The conv weight (C, 2C, 1, 1) in the fused kernel's k4-packed stage layout
+    (``mrp_compress_weight_pack``); cached on the module per weight version."""
+    from .aggregate import _ptr, _stream
     w = conv.weight
     key = (w.data_ptr(), w._version, w.device)
-    hit = getattr(conv, "_mrp_wt", None)
+    hit = getattr(conv, "_mrp_wp", None)
     if hit is not None and hit[0] == key:
         return hit[1]
-    wt = w.detach().reshape(w.shape[0], w.shape[1]).t().contiguous()
-    conv._mrp_wt = (key, wt)
-    return wt
+    C = w.shape[0]
+    src = w.detach().reshape(C, 2 * C).contiguous()
+    wp = torch.empty(2 * C * C, device=w.device, dtype=torch.float32)
+    with torch.cuda.device(w.device):
+        _lib.check(_lib.load_library().mrp_compress_weight_pack(_ptr(src), _ptr(wp), C, _stream(w.device)),
+                   "mrp_compress_weight_pack")
+    conv._mrp_wp = (key, wp)
+    return wp
+
+
+def fused_compress_supported(conv: torch.nn.Conv2d, x: torch.Tensor, csr) -> bool:
+    """Whether ``mrp_compress_film_fwd`` covers this layer: fp32 CUDA features, a plain 1x1
+    Conv2d(2C, C), complete graphs of 2..8 nodes, H W % 16 == 0, C % 128 == 0."""
+    if x.dim() != 4:
+        return False
+    n, C, H, W = x.shape
+    if (not x.is_cuda or x.dtype != torch.float32 or conv.kernel_size != (1, 1) or conv.groups != 1
+            or conv.stride != (1, 1) or conv.dilation != (1, 1) or conv.padding not in ((0, 0), "valid")
+            or tuple(conv.weight.shape[:2]) != (C, 2 * C) or conv.weight.dtype != torch.float32):
+        return False
+    return csr.graph_kind == _lib.GRAPH_COMPLETE and 2 <= csr.max_nodes <= 8 and (H * W) % 16 == 0 and C % 128 == 0
 
 
 def compress_film_fused(conv: torch.nn.Conv2d, x: torch.Tensor, gb, csr, mode: int):
@@ -78,13 +97,9 @@ def compress_film_fused(conv: torch.nn.Conv2d, x: torch.Tensor, gb, csr, mode: i
     the (N, 2C, H, W) concatenation never reaches HBM.  Forward only (no autograd).  Returns None
     when the kernel does not cover the shape (non-complete graphs, N > 8, P % 16, C % 128): the
     caller then runs the cat kernel + batched GEMM."""
+    if not fused_compress_supported(conv, x, csr):
+        return None
     n, C, H, W = x.shape
-    if (not x.is_cuda or x.dtype != torch.float32 or conv.kernel_size != (1, 1) or conv.groups != 1
-            or conv.stride != (1, 1) or conv.dilation != (1, 1) or conv.padding not in ((0, 0), "valid")
-            or tuple(conv.weight.shape[:2]) != (C, 2 * C) or conv.weight.dtype != torch.float32):
-        return None
-    if csr.graph_kind != _lib.GRAPH_COMPLETE or not 2 <= csr.max_nodes <= 8 or (H * W) % 16 or C % 128:
-        return None
     from .aggregate import _ptr, _stream, node_stride
     xs = node_stride(x)
     if xs is None:
@@ -102,7 +117,7 @@ def compress_film_fused(conv: torch.nn.Conv2d, x: torch.Tensor, gb, csr, mode: i
             with torch.cuda.device(x.device):
                 _lib.check(lib.mrp_film_gate(_ptr(gb), _ptr(gate), gb.numel(), _stream(x.device)), "mrp_film_gate")
             gb, mode = gate, mode & ~_lib.GB_LOGITS
-    wt = _weight_t(conv)
+    wt = _weight_packed(conv)
     bias = conv.bias.detach() if conv.bias is not None else None
     if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
         bias = bias.float().contiguous()

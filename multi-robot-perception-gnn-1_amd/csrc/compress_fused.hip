@@ -21,11 +21,24 @@
 // Supported: complete graphs (the reference topology, arithmetic edge ids) of N <= 8 nodes,
 // P % 16 == 0, C % 128 == 0, mean/sum FiLM modes (gamma/beta as logits or post-sigmoid).  Anything
 // else returns hipErrorNotSupported and the caller runs the unfused kernels (cat + library GEMM).
+//
+// Where the time goes (lab: tools/exp_cf_stamps.py, s_memtime around the barriers of one workgroup):
+// an fp32 MFMA holds its SIMD's instruction issue for its whole 32 cycles, so the producers' VALU does
+// not overlap the consumers' MFMAs — it is added to them.  A producer stage of 3.3k cycles alone took
+// 10.9–11.4k beside the MFMAs (its aggregate phase 1.15k -> 7.3k: about one producer instruction per
+// MFMA), against 9.0k cycles of MFMA-only stage.  Denser MFMA streams (b128 fragments for both
+// operands) run the consumers alone faster (0.99 vs 1.02 ms) and the whole kernel slower (1.35 vs
+// 1.26 ms at configs[1]).  Net: 1.19 ms against 1.24 ms for cat kernel + library GEMM at configs[1]
+// (32x32 planes) and slower than it on 8x8 planes, where models.py keeps the unfused path.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "mrp_gnn.h"
+
+#ifndef MRP_CF_WIDE_A
+#define MRP_CF_WIDE_A 0
+#endif
 
 namespace mrp_cf {
 
@@ -40,22 +53,41 @@ constexpr int KS = 16;         // input channels per stage (4 per producer wave)
 template <int NC>
 struct Geo {
   static constexpr int BM = 32 * NC;
-  static constexpr int WROW = BM + 16;                 // W stage row, padded: k rows 16 banks apart
   static constexpr int THREADS = 64 * (NC + kProducers);
   static constexpr int WF4 = 2 * KS * BM / 4 / (64 * kProducers);  // W float4 per producer lane per stage
 };
+
+// LDS stage layouts are "k4-packed": the 16 channels k = 4 k4 + lk of a stage are stored as [lk][...][k4],
+// so the four values one MFMA lane (k row lk) needs for the stage's four k-steps are one 16-byte
+// ds_read_b128 — 20 LDS reads per stage per consumer wave instead of 80 ds_read_b32.  A quarter-wave
+// (16 lanes of one lk) reads 256 contiguous bytes: no bank conflicts without padding.
+//   x / aggregate stage:  [node u][lk][pixel][k4]        (NT x 4 x 16 x 4 floats)
+//   W stage:              [half h][lk][m (BM)][k4]       (2 x 4 x BM x 4 floats)
+// The weight arrives pre-packed in HBM as [h][stage][lk][m (C)][k4] (mrp_compress_weight_pack), so a
+// producer's float4 load is exactly one LDS float4.
+// kPackB: the x / aggregate stages k4-packed too (one b128 per B fragment set) or plain [u][ch][pixel]
+// (four ds_read_b32).  Packed makes the MFMA stream denser, which starves the producer waves more
+// (an fp32 MFMA holds its SIMD's issue: lab stamps), so the plain layout is the faster combination.
+constexpr bool kPackB = false;
+// kWideA: the W fragments as one b128 per k4 set (1) or four ds_read_b32 from the same packed layout
+// (0, default: 1.19 vs 1.23 ms at configs[1] for the same reason as kPackB)
+constexpr bool kWideA = MRP_CF_WIDE_A;
+__device__ __forceinline__ int xk4(int u, int ch, int px) {
+  return kPackB ? ((u * 4 + (ch & 3)) * TP + px) * 4 + (ch >> 2) : (u * KS + ch) * TP + px;
+}
 
 struct Args {
   const float* x;
   int64_t xs;
   const float* gb;  // (E, C, 2)
-  const float* wt;  // (2C, C): conv weight transposed, k-major
+  const float* wt;  // the conv weight packed by mrp_compress_weight_pack: [2][C/16][4][C][4]
   const float* bias;
   float* y;
   int64_t ys;
   int32_t C, P, ntiles_p, ntiles_m, mode, logits, remap;
   int32_t debug;  // kernel lab only: 1 = producers skip their work, 2 = consumers skip the MFMAs,
-                  // 32 = no producer priority, 64 = BM 128 even where C allows 256
+                  // 32 = no producer priority, 64 = BM 256 where C allows it
+  long long* stamps;  // kernel lab only: s_memtime before/after the first 16 barriers of block 0, per wave
 };
 
 __device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
@@ -99,8 +131,8 @@ __device__ __forceinline__ float row_bcast(float v, int src) {
 
 template <int NT, int NC>
 struct Lds {
-  static constexpr int XS = NT * KS * TP;        // x stage  [node][ch][pix]
-  static constexpr int WS = 2 * KS * Geo<NC>::WROW;  // W stage  [half][k][m]
+  static constexpr int XS = NT * KS * TP;        // x stage  [node][lk][pix][k4]
+  static constexpr int WS = 2 * KS * Geo<NC>::BM;  // W stage  [half][lk][m][k4]
   static constexpr int BUF = 2 * XS + WS;        // x, aggregate, W
   static constexpr int TOTAL = 2 * BUF;          // double buffer
 };
@@ -112,12 +144,12 @@ struct Lds {
 // quarter of the W stage.  Consumer and producer waves share each SIMD: the MFMA pipe and the
 // VALU/memory work of the producer run concurrently (MI355X_MICROARCH.md, wave scheduling).  One
 // workgroup barrier per stage hands the double-buffered stage over.  The aggregate of a (graph, pixel
-// tile, stage) is recomputed by each of the C / BM workgroups of its output-channel column, so the
-// wider tile (NC = 8, BM = 256) halves the producers' work per MFMA.
+// tile, stage) is recomputed by each of the C / BM workgroups of its output-channel column; the wider
+// tile (NC = 8, BM = 256) halves that, but at one workgroup per CU it measured slower.
 template <int NT, int NC, bool FILM, bool LOGITS, bool MEAN>
 __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
   using L = Lds<NT, NC>;
-  constexpr int BM = Geo<NC>::BM, WROW = Geo<NC>::WROW, WF4 = Geo<NC>::WF4;
+  constexpr int BM = Geo<NC>::BM, WF4 = Geo<NC>::WF4;
   extern __shared__ f4 smem_f4[];
   float* smem = reinterpret_cast<float*>(smem_f4);
 
@@ -136,6 +168,15 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nstages = a.C / KS;
+  // lab stamps (a.stamps == nullptr in the product): shader-clock time around each barrier
+  const bool stamping = a.stamps != nullptr && blockIdx.x == 0;
+  int nbar = 0;
+  auto sync = [&]() {
+    if (stamping && nbar < 16 && lane == 0) a.stamps[w * 32 + 2 * nbar] = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (stamping && nbar < 16 && lane == 0) a.stamps[w * 32 + 2 * nbar + 1] = __builtin_amdgcn_s_memtime();
+    ++nbar;
+  };
 
   if (w >= NC) {
     // ------------------------------------------------------------------ producer
@@ -170,16 +211,18 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
     // The host guarantees every byte offset fits in 31 bits.
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.x + (int64_t)node0 * a.xs + p0), 0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.wt + m0), 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.wt + 4 * m0), 0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.gb != nullptr ? a.gb + ebase * a.C * 2 : a.x), 0, 0x7fffffff, 0x00020000);
     const uint32_t x_off = (uint32_t)(pch * a.P + px) * 4u;
+    // W float4 i of this lane: m = idx % BM, lk = (idx / BM) % 4, h = idx / (4 BM); in HBM at
+    // [h][stage][lk][m0 + m][0..3], the stage part going into the per-stage soffset
     uint32_t w_off[WF4];
 #pragma unroll
     for (int i = 0; i < WF4; ++i) {
       const int idx = pt_id + i * 256;
-      const int m4 = idx % (BM / 4), k = (idx / (BM / 4)) % KS, h = idx / (BM / 4 * KS);
-      w_off[i] = (uint32_t)((h * a.C + k) * a.C + 4 * m4) * 4u;
+      const int m = idx % BM, lk = (idx / BM) % 4, h = idx / (4 * BM);
+      w_off[i] = (uint32_t)(((h * (a.C / KS) * 4 + lk) * a.C + m) * 4) * 4u;
     }
     uint32_t g_off[GI];
 #pragma unroll
@@ -194,7 +237,7 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
       const int c0 = s * KS;
 #pragma unroll
       for (int i = 0; i < WF4; ++i)  // W stage: 2 halves x 16 k x BM m
-        R.wr[i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wr, w_off[i], c0 * a.C * 4, 0));
+        R.wr[i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wr, w_off[i], c0 * a.C * 4, 0));  // stage = 16 C floats
       // slots past the graph's NE edges reload the last edge (never read): no divergent branch around
       // the loads, so the compiler counts them exactly
 #pragma unroll
@@ -209,13 +252,14 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
       float* As = Xs + L::XS;
       float* Ws = As + L::XS;
 #pragma unroll
-      for (int u = 0; u < NT; ++u) Xs[(u * KS + pch) * TP + px] = X.xr[u];
+      for (int u = 0; u < NT; ++u) Xs[xk4(u, pch, px)] = X.xr[u];
 #pragma unroll
       for (int i = 0; i < WF4; ++i) {
         const int idx = pt_id + i * 256;
-        const int m4 = idx % (BM / 4), k = (idx / (BM / 4)) % KS, h = idx / (BM / 4 * KS);
-        *reinterpret_cast<f4*>(Ws + (h * KS + k) * WROW + 4 * m4) = R.wr[i];
+        const int m = idx % BM, lk = (idx / BM) % 4, h = idx / (4 * BM);
+        *reinterpret_cast<f4*>(Ws + ((h * 4 + lk) * BM + m) * 4) = R.wr[i];
       }
+      if (stamping && nbar < 16 && lane == 0) a.stamps[16 * 32 + w * 64 + 4 * nbar + 0] = __builtin_amdgcn_s_memtime();
       float gam[GI], bet[GI];
 #pragma unroll
       for (int i = 0; i < GI; ++i) {
@@ -225,41 +269,58 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
       // agg[v] = sum over u != v, ascending, of fl(fl(gamma_uv x_u) + beta_uv): gamma/beta of edge
       // e = u -> v (i-major ids, dgl/dataloader.py:88-95) sit in lane e % 16 of this channel's row,
       // slot e / 16, and reach every pixel lane by a DPP row broadcast (no LDS round trip)
+      // Under fp32 MFMA traffic a producer instruction that is not ready when the SIMD is free loses
+      // the slot to a 32-cycle MFMA (lab stamps: a producer stage of 3.2k cycles alone took 11.4k
+      // beside the MFMAs), so the stage is written for independent instructions back to back: the
+      // destinations go in groups of four, all products, then all + beta, then the four running sums
+      // interleaved (each sum still adds its terms in ascending source order).
       float sum[NT];
       float mn = __builtin_inff(), mx = 0.f;
+      constexpr int VG = NT < 4 ? NT : 4;
 #pragma unroll
-      for (int v = 0; v < NT; ++v) {
-        // all products, then all + beta, then the sum: a DPP instruction reading a VGPR written by
-        // the previous VALU instruction needs two wait states (s_nop), so no DPP op consumes the
-        // result right before it
-        float m[NT];
+      for (int v0 = 0; v0 < NT; v0 += VG) {
+        float m[VG][NT];
 #pragma unroll
-        for (int u = 0; u < NT; ++u) {
-          if (u == v) continue;
-          m[u] = X.xr[u];
-          if (FILM) {
-            const int e = u * (NT - 1) + (v < u ? v : v - 1);
-            m[u] = __fmul_rn(row_bcast(gam[e >> 4], e & 15), m[u]);
+        for (int vv = 0; vv < VG; ++vv) {
+          const int v = v0 + vv;
+#pragma unroll
+          for (int u = 0; u < NT; ++u) {
+            if (v >= NT || u == v) continue;
+            m[vv][u] = X.xr[u];
+            if (FILM) {
+              const int e = u * (NT - 1) + (v < u ? v : v - 1);
+              m[vv][u] = __fmul_rn(row_bcast(gam[e >> 4], e & 15), m[vv][u]);
+            }
           }
         }
         if (FILM) {
 #pragma unroll
-          for (int u = 0; u < NT; ++u) {
-            if (u == v) continue;
-            const int e = u * (NT - 1) + (v < u ? v : v - 1);
-            m[u] = __fadd_rn(row_bcast(bet[e >> 4], e & 15), m[u]);
+          for (int vv = 0; vv < VG; ++vv) {
+            const int v = v0 + vv;
+#pragma unroll
+            for (int u = 0; u < NT; ++u) {
+              if (v >= NT || u == v) continue;
+              const int e = u * (NT - 1) + (v < u ? v : v - 1);
+              m[vv][u] = __fadd_rn(row_bcast(bet[e >> 4], e & 15), m[vv][u]);
+            }
           }
         }
-        float acc = 0.f;
+        float acc[VG];
 #pragma unroll
-        for (int u = 0; u < NT; ++u) {
-          if (u == v) continue;
-          acc = __fadd_rn(acc, m[u]);
-        }
-        sum[v] = acc;
-        if (MEAN && NT > 2) {
-          mn = fminf(mn, __builtin_fabsf(acc));
-          mx = fmaxf(mx, __builtin_fabsf(acc));
+        for (int vv = 0; vv < VG; ++vv) acc[vv] = 0.f;
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+#pragma unroll
+          for (int vv = 0; vv < VG; ++vv)
+            if (v0 + vv < NT && u != v0 + vv) acc[vv] = __fadd_rn(acc[vv], m[vv][u]);
+#pragma unroll
+        for (int vv = 0; vv < VG; ++vv) {
+          if (v0 + vv >= NT) continue;
+          sum[v0 + vv] = acc[vv];
+          if (MEAN && NT > 2) {
+            mn = fminf(mn, __builtin_fabsf(acc[vv]));
+            mx = fmaxf(mx, __builtin_fabsf(acc[vv]));
+          }
         }
       }
       if (MEAN && NT > 2) {
@@ -272,7 +333,8 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
         }
       }
 #pragma unroll
-      for (int v = 0; v < NT; ++v) As[(v * KS + pch) * TP + px] = sum[v];
+      for (int v = 0; v < NT; ++v) As[xk4(v, pch, px)] = sum[v];
+      if (stamping && nbar < 16 && lane == 0) a.stamps[16 * 32 + w * 64 + 4 * nbar + 1] = __builtin_amdgcn_s_memtime();
     };
     // stage t: x in register set t & 1, LDS buffer t & 1.  nstages is a multiple of 8 (C % 128 == 0).
     // The loop body has no conditional loads (stage indices are clamped instead): with a path that
@@ -285,22 +347,22 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
     issue_wg(WG, 1);
     issue_x(X0, min(2, last));
     if (a.debug & 1) {  // lab: consumers only
-      for (int s = 0; s < nstages; ++s) __syncthreads();
+      for (int s = 0; s < nstages; ++s) sync();
       return;
     }
     for (int s = 0; s < nstages - 2; s += 2) {
-      __syncthreads();  // barrier #s: stage s complete in LDS, stage s-1 consumed
+      sync();  // barrier #s: stage s complete in LDS, stage s-1 consumed
       produce(X1, WG, 1);  // stage s+1
       issue_wg(WG, s + 2);
       issue_x(X1, s + 3);
-      __syncthreads();  // barrier #(s+1)
+      sync();  // barrier #(s+1)
       produce(X0, WG, 0);  // stage s+2
       issue_wg(WG, min(s + 3, last));
       issue_x(X0, min(s + 4, last));
     }
-    __syncthreads();  // barrier #(nstages-2)
+    sync();  // barrier #(nstages-2)
     produce(X1, WG, 1);  // the last stage
-    __syncthreads();  // barrier #(nstages-1)
+    sync();  // barrier #(nstages-1)
     return;
   }
 
@@ -312,27 +374,45 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
     for (int j = 0; j < NT; ++j) acc[mb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int lk = lane >> 4, lc = lane & 15;
   for (int s = 0; s < nstages; ++s) {
-    __syncthreads();  // stage s is in LDS; the producers now fill stage s+1 in the other buffer
+    sync();  // stage s is in LDS; the producers now fill stage s+1 in the other buffer
     const float* Xs = smem + (s & 1) * L::BUF;
     const float* As = Xs + L::XS;
     const float* Ws = As + L::XS;
     if (a.debug & 2) continue;  // lab: producers only
 #pragma unroll
-    for (int k4 = 0; k4 < KS / 4; ++k4) {
-      const int k = 4 * k4 + lk;
+    for (int h = 0; h < 2; ++h) {
+      const f4* B4 = reinterpret_cast<const f4*>(h == 0 ? Xs : As);
+      const f4* A4 = reinterpret_cast<const f4*>(Ws);
+      f4 af[2], bf[NT];
+      if (kWideA) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const float* Bsrc = h == 0 ? Xs : As;
-        float af[2];
+        for (int mb = 0; mb < 2; ++mb) af[mb] = A4[(h * 4 + lk) * BM + 32 * w + 16 * mb + lc];
+      } else {
+        const float* A1 = reinterpret_cast<const float*>(A4);
 #pragma unroll
-        for (int mb = 0; mb < 2; ++mb) af[mb] = Ws[(h * KS + k) * WROW + 32 * w + 16 * mb + lc];
+        for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          const float bf = Bsrc[(j * KS + k) * TP + lc];
-#pragma unroll
-          for (int mb = 0; mb < 2; ++mb) acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mb], bf, acc[mb][j], 0, 0, 0);
-        }
+          for (int k4 = 0; k4 < 4; ++k4) af[mb][k4] = A1[((h * 4 + lk) * BM + 32 * w + 16 * mb + lc) * 4 + k4];
       }
+      if (kPackB) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bf[j] = B4[(j * 4 + lk) * TP + lc];
+      } else {
+        const float* B1 = reinterpret_cast<const float*>(B4);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int k4 = 0; k4 < 4; ++k4) bf[j][k4] = B1[(j * KS + 4 * k4 + lk) * TP + lc];
+      }
+      // k-step k4 covers channels 4 k4 + (0..3) (lane row lk); consecutive MFMAs use different
+      // accumulators, so no dependent issue back to back
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int mb = 0; mb < 2; ++mb)
+            acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mb][k4], bf[j][k4], acc[mb][j], 0, 0, 0);
     }
   }
 
@@ -362,11 +442,27 @@ __global__ void __launch_bounds__(256) film_gate(const float4* __restrict__ z, f
   }
 }
 
+// wp[h][s][lk][m][k4] = w[m][h C + 16 s + 4 k4 + lk]: the (C, 2C) conv weight in the k4-packed stage
+// layout above.  One thread per output float4.
+__global__ void __launch_bounds__(256) weight_pack(const float* __restrict__ w, f4* __restrict__ wp, int32_t C) {
+  const int64_t n4 = (int64_t)2 * C * C / 4;  // float4 of wp
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i % C;
+    const int64_t rest = i / C;  // (h, s, lk)
+    const int lk = (int)(rest % 4);
+    const int64_t hs = rest / 4;  // h * (C / 16) + s
+    const int64_t h = hs / (C / KS), st = hs % (C / KS);
+    const float* src = w + m * 2 * C + h * C + st * KS + lk;
+    wp[i] = f4{src[0], src[4], src[8], src[12]};
+  }
+}
+
 }  // namespace mrp_cf
 
 namespace {
 
 int mrp_cf_debug = 0;
+long long* mrp_cf_stamps = nullptr;
 
 template <int NT, int NC, bool FILM, bool LOGITS, bool MEAN>
 hipError_t launch_mode(const mrp_cf::Args& a, int64_t grid, hipStream_t st) {
@@ -390,10 +486,11 @@ hipError_t launch_nc(const mrp_cf::Args& a, int64_t grid, hipStream_t st) {
   return mean ? launch_mode<NT, NC, true, false, true>(a, grid, st) : launch_mode<NT, NC, true, false, false>(a, grid, st);
 }
 
-// BM = 256 output channels per workgroup when C allows it (and the lab hook does not force 128)
+// BM = 128 output channels per workgroup (two workgroups per CU); BM = 256 (one per CU, half the
+// redundant aggregation per MFMA) only through the lab hook: 1.25 vs 1.19 ms at configs[1]
 template <int NT>
 hipError_t launch(mrp_cf::Args a, int32_t num_graphs, hipStream_t st) {
-  const int nc = (a.C % 256 == 0 && !(a.debug & 64)) ? 8 : 4;
+  const int nc = (a.C % 256 == 0 && (a.debug & 64)) ? 8 : 4;
   a.ntiles_m = a.C / (32 * nc);
   const int64_t grid = (int64_t)num_graphs * a.ntiles_p * a.ntiles_m;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
@@ -402,6 +499,16 @@ hipError_t launch(mrp_cf::Args a, int32_t num_graphs, hipStream_t st) {
 }
 
 }  // namespace
+
+extern "C" int mrp_compress_weight_pack(const float* w, float* wp, int32_t C, void* stream) {
+  if (C <= 0 || C % mrp_cf::KS != 0 || w == nullptr || wp == nullptr || (reinterpret_cast<uintptr_t>(wp) & 15))
+    return hipErrorInvalidValue;
+  const int64_t n4 = (int64_t)2 * C * C / 4;
+  const int64_t blocks = (n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096;
+  hipLaunchKernelGGL(mrp_cf::weight_pack, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), w,
+                     reinterpret_cast<mrp_cf::f4*>(wp), C);
+  return hipGetLastError();
+}
 
 extern "C" int mrp_film_gate(const float* z, float* gb, int64_t n, void* stream) {
   if (n < 0 || n % 4 != 0) return hipErrorInvalidValue;
@@ -417,6 +524,7 @@ extern "C" int mrp_film_gate(const float* z, float* gb, int64_t n, void* stream)
 
 // kernel-lab hook (tools/exp_compress_fused.py): not part of the ABI header
 extern "C" void mrp_compress_film_debug(int mode) { mrp_cf_debug = mode; }
+extern "C" void mrp_compress_film_debug_stamps(long long* device_buffer) { mrp_cf_stamps = device_buffer; }
 
 extern "C" int mrp_compress_film_fwd(const float* x, int64_t x_node_stride, const float* gb, int32_t num_graphs,
                                      int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges,
@@ -455,6 +563,7 @@ extern "C" int mrp_compress_film_fwd(const float* x, int64_t x_node_stride, cons
   a.mode = mode;
   a.logits = logits;
   a.debug = mrp_cf_debug;
+  a.stamps = mrp_cf_stamps;
   hipStream_t st = static_cast<hipStream_t>(stream);
   switch (max_nodes) {
     case 2: return launch<2>(a, num_graphs, st);

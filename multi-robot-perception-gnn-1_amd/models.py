@@ -34,7 +34,7 @@ import torch
 import torch.nn as nn
 
 from .aggregate import film_mean, film_mean_cat, film_mean_mix, film_mean_residual
-from .compress import compress_1x1, compress_film_fused
+from .compress import compress_1x1, compress_film_fused, fused_compress_supported
 from .encoder import edge_logits
 
 
@@ -137,7 +137,8 @@ class GCN(nn.Module):
         x = feats
         if (x.is_cuda and self._return_mode() != "input" and not torch.is_grad_enabled()
                 and _opt(self.opt, "gcn_mode", "film_mean") != "copy_mean"
-                and fused_compress_enabled(x.shape[-2] * x.shape[-1])):
+                and fused_compress_enabled(x.shape[-2] * x.shape[-1])
+                and fused_compress_supported(conv, x, g.csr(x.device))):
             mode = _lib_modes()[_opt(self.opt, "gcn_mode", "film_mean")]
             z = self.edge_encoder.logits(g.edata["pose"])
             y = compress_film_fused(conv, x, z, g.csr(x.device), mode | _lib_logits())

@@ -115,3 +115,19 @@ def test_stack_eval_takes_fused_path(cuda_device):
     # with autograd the stack runs the unfused kernels (the fused kernel has no backward)
     out = net(g, x.clone().requires_grad_(True))
     assert out.grad_fn is not None
+
+
+@pytest.mark.parametrize("C", [16, 128, 256])
+def test_weight_pack_layout(cuda_device, C):
+    """mrp_compress_weight_pack: wp[h][s][lk][m][k4] = w[m][h C + 16 s + 4 k4 + lk] (include/mrp_gnn.h)."""
+    from mrp_gnn_amd.compress import _weight_packed
+    conv = torch.nn.Conv2d(2 * C, C, 1).to(cuda_device)
+    wp = _weight_packed(conv).cpu()
+    w = conv.weight.detach().cpu().reshape(C, 2, C // 16, 4, 4)  # [m][h][s][k4][lk]
+    ref = w.permute(1, 2, 4, 0, 3).reshape(-1)
+    assert torch.equal(wp, ref)
+    # cached per weight version; an in-place update repacks
+    assert _weight_packed(conv) is _weight_packed(conv)
+    with torch.no_grad():
+        conv.weight.mul_(2)
+    assert torch.equal(_weight_packed(conv).cpu(), ref * 2)

@@ -35,9 +35,9 @@ for name, (B, N, C, H) in {"cfg1": (16, 8, 512, 32), "cfg2": (32, 8, 1280, 8), "
         lib.mrp_compress_film_debug(32)
         t_noprio = time_launches([lambda: compress_film_fused(conv, x, z, csr, MODE)], 20, dev)
         lib.mrp_compress_film_debug(64)
-        t_bm128 = time_launches([lambda: compress_film_fused(conv, x, z, csr, MODE)], 20, dev)
+        t_bm256 = time_launches([lambda: compress_film_fused(conv, x, z, csr, MODE)], 20, dev)
         lib.mrp_compress_film_debug(0)
-        print(f"{name}: fused without producer priority {t_noprio * 1e6:8.1f} us, with BM 128 {t_bm128 * 1e6:8.1f} us",
+        print(f"{name}: fused without producer priority {t_noprio * 1e6:8.1f} us, with BM 256 {t_bm256 * 1e6:8.1f} us",
               flush=True)
         print(f"{name}: lab consumers-only {lab[0] * 1e6:8.1f} us ({flop / lab[0] / 1e12:6.1f} TF/s)  "
               f"producers-only {lab[1] * 1e6:8.1f} us", flush=True)

@@ -1,6 +1,6 @@
 """Profiling driver (not product code): the fused aggregation + compress kernel at the configs[1]
 shape, ``iters`` launches with a kernel-lab debug mode (0 = product, 1 = consumers only, 2 = producers
-only, 64 = BM 128), for one ``rocprofv3 --pmc`` pass.  Usage: python tools/prof_compress_fused.py mode [iters]"""
+only, 64 = BM 256), for one ``rocprofv3 --pmc`` pass.  Usage: python tools/prof_compress_fused.py mode [iters]"""
 import ctypes
 import os
 import sys
