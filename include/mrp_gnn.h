@@ -302,7 +302,8 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * plane of a MRP_GRAPH_REGULAR forward over several workgroups, 0 keeps whole planes. */
 int mrp_tuning_set(const char* name, int32_t value);
 
-/* Library identification: ABI version (incremented on signature changes). */
+/* Library identification: ABI version (incremented on signature changes; 11 = this header: the
+ * epilogue entry points of v10 plus mrp_compress_film_fwd, mrp_compress_weight_pack, mrp_film_gate). */
 int mrp_abi_version(void);
 
 /* Human-readable text for a return code (static storage). */
