@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "fast_div.hpp"
 #include "mrp_gnn.h"
 
 #ifndef MRP_CF_WIDE_A
@@ -92,21 +93,8 @@ struct Args {
 
 __device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
 
-// x / D correctly rounded (== the IEEE division the oracle and the other kernels use) in three
-// instructions: q0 = x * RN(1/D), r = fma(-q0, D, x) (exact), q = fma(r, RN(1/D), q0).  Checked
-// exhaustively over all 2^32 fp32 x for D = 2..15 (tools/check_div_const.c): equal except for
-// |x| < 2^-124, +-0 and +-inf, which take the IEEE division.
-// The caller checks the range once for a whole set of quotients (div_fast_ok) and redoes the set
-// with the IEEE division when any lane is out of it, so the fast path has no branch per quotient.
-template <int D>
-__device__ __forceinline__ float div_fast(float x) {
-  constexpr float y = 1.0f / (float)D;
-  const float q0 = __fmul_rn(x, y);
-  const float r = __builtin_fmaf(-q0, (float)D, x);
-  return __builtin_fmaf(r, y, q0);
-}
-// min |x| >= 2^-124 and max |x| < inf (NaN inputs give NaN either way)
-__device__ __forceinline__ bool div_fast_ok(float mn, float mx) { return mn >= 0x1p-124f && mx < __builtin_inff(); }
+using mrp_math::div_fast;     // fast_div.hpp: the exact three-instruction x / (N - 1)
+using mrp_math::div_fast_ok;
 
 __device__ __forceinline__ const float* at_bytes(const float* base, uint32_t off) {
   return reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + off);

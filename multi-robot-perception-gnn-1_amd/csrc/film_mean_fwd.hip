@@ -28,6 +28,13 @@ hipError_t launch_fwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
     if (a.kdeg >= 5 && a.kdeg <= 8) return launch_fwd_regular<NT, 8>(a, g, st);
   }
   const size_t lds = lds_fwd<NT>(g.cpb);
+  if constexpr (COMPLETE && NT >= 2 && NT <= 8) {
+    // the reference's own configuration: mode and mean divisor compile-time (film_fwd MODE)
+    if (g.vec == 4 && a.mode == MRP_AGG_FILM_MEAN) {
+      MRP_LAUNCH((mrp::film_fwd<NT, 4, true, MRP_AGG_FILM_MEAN>), lds);
+      return hipGetLastError();
+    }
+  }
   if (g.vec == 4)
     MRP_LAUNCH((mrp::film_fwd<NT, 4, COMPLETE>), lds);
   else if (g.vec == 2)

@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "fast_div.hpp"
 #include "mrp_gnn.h"
 
 namespace mrp {
@@ -374,10 +375,14 @@ __device__ __forceinline__ void complete_rest(const AggArgs& a, int64_t ebase, i
 // ---------------------------------------------------------------------------
 // Forward.  out[v] = reduce_{e=(u->v)} (gamma_e * x_u + beta_e), zero if deg v == 0.
 // ---------------------------------------------------------------------------
-template <int NT, int VEC, bool COMPLETE>
+// MODE >= 0: the FiLM mode as a compile-time constant (the hot path: COMPLETE, MRP_AGG_FILM_MEAN,
+// N <= 8): no per-term select between the modes, and the mean's division by N - 1 as the exact
+// three-instruction quotient (fast_div.hpp) for a whole slice at once.  MODE = -1: mode at run time.
+template <int NT, int VEC, bool COMPLETE, int MODE = -1>
 __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
+  constexpr bool kBatchDiv = COMPLETE && MODE == MRP_AGG_FILM_MEAN && NT >= 2;
   extern __shared__ float4 smem_f4[];
   float* smem = reinterpret_cast<float*>(smem_f4);
   float* Ga = smem;
@@ -441,8 +446,8 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   __syncthreads();
   if (!active) return;
 
-  const bool film = a.mode != MRP_AGG_COPY_MEAN;
-  const bool mean = a.mode != MRP_AGG_FILM_SUM;
+  const bool film = MODE >= 0 ? MODE != MRP_AGG_COPY_MEAN : a.mode != MRP_AGG_COPY_MEAN;
+  const bool mean = MODE >= 0 ? MODE != MRP_AGG_FILM_SUM : a.mode != MRP_AGG_FILM_SUM;
   // CSR: neighbour masks and in-degrees are channel-independent -> wave-uniform; read them from LDS
   // once into scalar registers instead of once per slice
   unsigned emv[COMPLETE ? 1 : NT];
@@ -464,6 +469,10 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
     asm volatile("" : "+v"(tile));
     const float* A = Ga + tile;
     const float* Bt = Gb + tile;
+    // kBatchDiv: the sums of a group of VG destinations are divided as one set (one range check)
+    constexpr int VG = kBatchDiv ? (NT < 4 ? NT : 4) : 1;
+    Frag<VEC> accs[VG];
+    float mn = __builtin_inff(), mx = 0.f;
 #pragma unroll
     for (int v = 0; v < NT; ++v) {
       if (!COMPLETE && v >= n) break;
@@ -495,6 +504,41 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
           }
         }
       }
+      if constexpr (kBatchDiv) {
+        accs[v % VG] = acc;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          mn = fminf(mn, __builtin_fabsf(acc.v[k]));
+          mx = fmaxf(mx, __builtin_fabsf(acc.v[k]));
+        }
+        if (v % VG != VG - 1 && v != NT - 1) continue;
+        const int v0 = v - v % VG;
+        if (__builtin_expect(!mrp_math::div_fast_ok(mn, mx), 0)) {
+#pragma unroll
+          for (int i = 0; i < VG; ++i)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) accs[i].v[k] = accs[i].v[k] / (float)(NT - 1);
+        } else {
+#pragma unroll
+          for (int i = 0; i < VG; ++i)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) accs[i].v[k] = mrp_math::div_fast<NT - 1>(accs[i].v[k]);
+        }
+        mn = __builtin_inff();
+        mx = 0.f;
+#pragma unroll
+        for (int i = 0; i < VG; ++i) {
+          if (v0 + i > v) break;
+          if (a.epi) {
+            float xself[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) xself[k] = xv[k][v0 + i];
+            apply_epilogue<VEC>(a, accs[i].v, xself, node0 + v0 + i, c, off);
+          }
+          store_frag<VEC, true>(at_bytes(ob + (int64_t)(v0 + i) * a.os, lane_off), accs[i]);
+        }
+        continue;
+      }
       float d;
       if constexpr (COMPLETE)
         d = (float)(NT - 1);
@@ -512,6 +556,7 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
       }
       store_frag<VEC, true>(at_bytes(ob + (int64_t)v * a.os, lane_off), acc);
     }
+
     if (a.xc != nullptr) {
       // cat((x, aggregate), 1): the slices of x are in registers already; writing them here saves
       // the separate copy's read of x

@@ -98,6 +98,17 @@ def main():
         mrp.film_mean_forward_into(g.ndata["image"], z, csr, MODE, out)
     torch.cuda.synchronize()
     del g, z, csr, out
+    if what == "fwdall":  # the forward at every config shape, default geometry
+        for name in ("north_star", "cfg1", "cfg2", "cfg3", "cfg4"):
+            sweep("fwd", name, fwd_time, {"fwd_cap": [16]})
+        return
+    if what == "capfwd":  # small workgroups (round 2: a 1-float4-per-thread copy streams at 82 %)
+        for name in ("north_star", "cfg2", "cfg3"):
+            sweep("fwd", name, fwd_time, {"fwd_cap": [1, 2, 4, 8, 16]})
+        sweep("fwd", "north_star", fwd_time, {"fwd_lo": [16, 32], "fwd_hi": [16, 32, 64], "fwd_cap": [1, 2, 4]})
+        sweep("bwd", "cfg2", bwd_time, {"bwd_fused_cap": [1, 2, 4, 8]})
+        sweep("bwd", "cfg3", bwd_time, {"bwd_fused_cap": [1, 2, 4, 8]})
+        return
     if what == "regbwd":
         sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [1, 2], "bwd_regular_lanes": [8, 16, 32],
                                         "bwd_regular_slices": [0, 1, 2, 4]})
