@@ -98,7 +98,7 @@ def alg_bytes_bwd(Nt, E, C, P):
 
 
 def time_launches(launches, iters, device):
-    """Mean duration of one launch, HIP events on the launch stream; ``launches`` are closures over
+    """Duration of one launch (median over 5 graph replays), HIP events on the launch stream; ``launches`` are closures over
     distinct buffer sets, run round-robin.  The ``iters`` launches are captured once in a HIP graph
     and the events bracket its replay, so a short kernel is timed back to back on the device rather
     than at the rate Python can issue ctypes calls (~15-20 us per call: more than a small config's
@@ -115,14 +115,20 @@ def time_launches(launches, iters, device):
     graph.replay()  # warm
     torch.cuda.synchronize(device)
     stream = torch.cuda.current_stream(device)
-    start = torch.cuda.Event(enable_timing=True)
-    end = torch.cuda.Event(enable_timing=True)
-    start.record(stream)
-    graph.replay()
-    end.record(stream)
-    end.synchronize()
+    # median of 5 replays: single replays of the same launches differ by up to ~10 % box to box
+    # (clock and power state), which one replay would report as a kernel difference
+    times = []
+    for _ in range(5):
+        start = torch.cuda.Event(enable_timing=True)
+        end = torch.cuda.Event(enable_timing=True)
+        start.record(stream)
+        graph.replay()
+        end.record(stream)
+        end.synchronize()
+        times.append(start.elapsed_time(end))
     del graph
-    return start.elapsed_time(end) / iters * 1e-3  # seconds
+    times.sort()
+    return times[2] / iters * 1e-3  # seconds
 
 
 def roofline(kernel, bytes_launch, t, traffic=None, traffic_src=None, **extra):

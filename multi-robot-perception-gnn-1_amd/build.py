@@ -15,7 +15,7 @@ SOURCES = [os.path.join(PKG_DIR, "csrc", f) for f in ("film_mean_fwd.hip", "film
                                                     "compress_fused.hip")]
 OBJ_DIR = os.path.join(PKG_DIR, "build")
 HEADERS = [os.path.join(REPO, "include", "mrp_gnn.h")] + [os.path.join(PKG_DIR, "csrc", h) for h in (
-    "film_mean_kernels.hpp", "film_mean_bwd_launch.hpp", "fast_div.hpp")]
+    "film_mean_kernels.hpp", "film_mean_bwd_launch.hpp", "fast_math.hpp")]
 OUT = os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
 ARCH = os.environ.get("MRP_OFFLOAD_ARCH", "gfx950")
 

@@ -34,7 +34,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "fast_div.hpp"
+#include "fast_math.hpp"
 #include "mrp_gnn.h"
 
 #ifndef MRP_CF_WIDE_A
@@ -91,9 +91,9 @@ struct Args {
   long long* stamps;  // kernel lab only: s_memtime before/after the first 16 barriers of block 0, per wave
 };
 
-__device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
+__device__ __forceinline__ float sigmoidf(float z) { return mrp_math::sigmoid(z); }  // the aggregation kernels' own
 
-using mrp_math::div_fast;     // fast_div.hpp: the exact three-instruction x / (N - 1)
+using mrp_math::div_fast;     // fast_math.hpp: the exact three-instruction x / (N - 1)
 using mrp_math::div_fast_ok;
 
 __device__ __forceinline__ const float* at_bytes(const float* base, uint32_t off) {
@@ -420,7 +420,7 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
   }
 }
 
-// gamma/beta = sigmoid(z), the aggregation kernels' own expression (film_mean_kernels.hpp sigmoidf):
+// gamma/beta = sigmoid(z), the aggregation kernels' own expression (fast_math.hpp):
 // the fused kernel then reads post-sigmoid pairs instead of evaluating 2 x NE sigmoids per channel in
 // every workgroup of a (graph, channel) column
 __global__ void __launch_bounds__(256) film_gate(const float4* __restrict__ z, float4* __restrict__ g, int64_t n4) {

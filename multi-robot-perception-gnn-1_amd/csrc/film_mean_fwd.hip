@@ -34,6 +34,10 @@ hipError_t launch_fwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
       MRP_LAUNCH((mrp::film_fwd<NT, 4, true, MRP_AGG_FILM_MEAN>), lds);
       return hipGetLastError();
     }
+    if (g.vec == 2 && a.mode == MRP_AGG_FILM_MEAN) {
+      MRP_LAUNCH((mrp::film_fwd<NT, 2, true, MRP_AGG_FILM_MEAN>), lds);
+      return hipGetLastError();
+    }
   }
   if (g.vec == 4)
     MRP_LAUNCH((mrp::film_fwd<NT, 4, COMPLETE>), lds);
@@ -78,6 +82,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"fwd_lo", &t.fwd_lo, 1, 256},
       {"fwd_hi", &t.fwd_hi, 1, 256},
       {"fwd_cap", &t.fwd_cap, 1, 16},
+      {"fwd_vec2_below", &t.fwd_vec2_below, 0, 1 << 20},
       {"fwd_regular_split", &t.fwd_regular_split, 0, 1},
       {"fwd_regular_lo", &t.fwd_regular_lo, 1, 256},
       {"fwd_regular_hi", &t.fwd_regular_hi, 1, 256},
@@ -133,8 +138,9 @@ int film_fwd_impl(const float* x, int64_t x_node_stride, const float* gb, const 
   const bool regular = kdeg >= 1 && kdeg <= 8;
   // 16-byte slices beat 8-byte ones at every measured size (tools/kernel_lab.hip product sweep)
   const Tuning& tu = tuning();
+  const int fvec = vec4 ? (P < tu.fwd_vec2_below ? 2 : 4) : 1;
   Geometry g = regular ? make_geometry(C, P, vec4 ? 4 : 1, tu.fwd_regular_lo, tu.fwd_regular_hi, tu.fwd_regular_cap)
-                       : make_geometry(C, P, vec4 ? 4 : 1, tu.fwd_lo, tu.fwd_hi, tu.fwd_cap);
+                       : make_geometry(C, P, fvec, tu.fwd_lo, tu.fwd_hi, tu.fwd_cap);
   // COMPLETE graphs: one slice per lane, the plane split over ceil(PV / lpc) workgroups (their
   // prologue is one round of independent gamma/beta loads, hidden under the first slice).  CSR
   // graphs keep whole planes: their prologue walks the CSR (dependent loads) and a split repeats it

@@ -36,7 +36,7 @@
 #include <algorithm>
 #include <type_traits>
 
-#include "fast_div.hpp"
+#include "fast_math.hpp"
 #include "mrp_gnn.h"
 
 namespace mrp {
@@ -112,7 +112,7 @@ __device__ __forceinline__ void apply_epilogue(const AggArgs& a, float* acc, con
   }
 }
 
-__device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
+__device__ __forceinline__ float sigmoidf(float z) { return mrp_math::sigmoid(z); }  // fast_math.hpp
 
 // d/dz of gamma/beta = sigmoid(z): grad * s * (1 - s)
 __device__ __forceinline__ float2 sigmoid_backward(float2 grad, float2 z) {
@@ -324,8 +324,9 @@ __device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, 
         if (a.mode == MRP_AGG_COPY_MEAN) {
           val = make_float2(1.f, 0.f);
         } else {
+          // raw value: the sigmoid (logits) is applied in complete_store, so the caller's feature
+          // loads issue before this load has to return
           val = *reinterpret_cast<const float2*>(a.gb + (complete_eid(ebase, NT, u, v) * a.C + c) * 2);
-          if (a.logits) val = make_float2(sigmoidf(val.x), sigmoidf(val.y));
         }
       }
     }
@@ -342,6 +343,7 @@ __device__ __forceinline__ void complete_store(const AggArgs& a, int base, const
   const int tot = a.cpb * S;
   const float s = ((BWD && a.mode != MRP_AGG_FILM_SUM && NT > 1) ? 1.f / (float)(NT - 1) : 1.f) *
                   (BWD ? a.agg_scale : 1.f);
+  const bool act = a.logits && a.mode != MRP_AGG_COPY_MEAN;
 #pragma unroll
   for (int r = 0; r < CompleteSlots<NT>::kPer; ++r) {
     const int t = base + threadIdx.x + r * blockDim.x;
@@ -349,12 +351,15 @@ __device__ __forceinline__ void complete_store(const AggArgs& a, int base, const
       int cl, slot;
       split_channel(a, t, cl, slot);
       const int v = slot / NT, u = slot - v * NT;
+      float2 w = reg[r];
+      // (diagonal and out-of-range slots hold 0 and turn into 0.5 here: never read)
+      if (act) w = make_float2(sigmoidf(w.x), sigmoidf(w.y));
       if (BWD) {
-        Ga[cl * SZ + u * NTP + v] = s * reg[r].x;
-        if (Sg != nullptr) Sg[t] = reg[r];  // sigmoid(z) of slot (cl, v, u), reused by the epilogue
+        Ga[cl * SZ + u * NTP + v] = s * w.x;
+        if (Sg != nullptr) Sg[t] = w;  // sigmoid(z) of slot (cl, v, u), reused by the epilogue
       } else {
-        Ga[cl * SZ + v * NTP + u] = reg[r].x;
-        Gb[cl * SZ + v * NTP + u] = reg[r].y;
+        Ga[cl * SZ + v * NTP + u] = w.x;
+        Gb[cl * SZ + v * NTP + u] = w.y;
       }
     }
   }
@@ -377,7 +382,7 @@ __device__ __forceinline__ void complete_rest(const AggArgs& a, int64_t ebase, i
 // ---------------------------------------------------------------------------
 // MODE >= 0: the FiLM mode as a compile-time constant (the hot path: COMPLETE, MRP_AGG_FILM_MEAN,
 // N <= 8): no per-term select between the modes, and the mean's division by N - 1 as the exact
-// three-instruction quotient (fast_div.hpp) for a whole slice at once.  MODE = -1: mode at run time.
+// three-instruction quotient (fast_math.hpp) for a whole slice at once.  MODE = -1: mode at run time.
 template <int NT, int VEC, bool COMPLETE, int MODE = -1>
 __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   constexpr int SZ = Tile<NT>::SZ;
@@ -1343,6 +1348,7 @@ struct Geometry {
 // Launch geometry knobs (defaults = the measured optima; mrp_tuning_set changes them for lab sweeps).
 struct Tuning {
   int fwd_lo = 16, fwd_hi = 64, fwd_cap = 16;  // film_fwd: lanes per plane in [lo, hi], <= cap channels
+  int fwd_vec2_below = 0;  // film_fwd: 8-byte slices for planes of fewer than this many pixels (lab knob)
   // film_fwd_regular: whole planes, 32 lanes each (k-NN(4) N=16 C=1024 16x16, B=8: 54.1 us against
   // 57.0 us split over 2 workgroups with 32 lanes; tools/sweep_geometry.py)
   int fwd_regular_split = 0;

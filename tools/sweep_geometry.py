@@ -98,6 +98,10 @@ def main():
         mrp.film_mean_forward_into(g.ndata["image"], z, csr, MODE, out)
     torch.cuda.synchronize()
     del g, z, csr, out
+    if what == "vec2":  # 8-byte slices on small planes (fewer registers, more waves)
+        for name in ("cfg2", "cfg3", "cfg4", "cfg1"):
+            sweep("fwd", name, fwd_time, {"fwd_vec2_below": [0, 1 << 20], "fwd_lo": [16, 32]})
+        return
     if what == "fwdall":  # the forward at every config shape, default geometry
         for name in ("north_star", "cfg1", "cfg2", "cfg3", "cfg4"):
             sweep("fwd", name, fwd_time, {"fwd_cap": [16]})
