@@ -106,6 +106,15 @@ def main():
         for name in ("north_star", "cfg1", "cfg2", "cfg3", "cfg4"):
             sweep("fwd", name, fwd_time, {"fwd_cap": [16]})
         return
+    if what == "cfg4fwd":  # repeated k-NN forward timings (A/B between library builds)
+        for _ in range(3):
+            sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0]})
+        return
+    if what == "bwdall":  # the backward at every config shape, default geometry
+        for name in ("north_star", "cfg1", "cfg2", "cfg3"):
+            sweep("bwd", name, bwd_time, {"bwd_fused_cap": [8]})
+        sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [2]})
+        return
     if what == "capfwd":  # small workgroups (round 2: a 1-float4-per-thread copy streams at 82 %)
         for name in ("north_star", "cfg2", "cfg3"):
             sweep("fwd", name, fwd_time, {"fwd_cap": [1, 2, 4, 8, 16]})
