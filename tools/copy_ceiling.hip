@@ -58,14 +58,15 @@ __global__ void __launch_bounds__(256) gather_nt(const f4* __restrict__ in, f4* 
   }
 }
 
+template <int NT>
 static double time_gather(int nsets, int iters, const std::vector<void*>& bufs, size_t n4, size_t node4) {
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  const size_t graph_items = 8 * node4 / 8;  // per graph: node4 float4 per node... items = node4
-  const unsigned grid = (unsigned)((n4 / 8 + 255) / 256);
+  const size_t graph_items = node4;  // per graph: (channel, slice) items = float4 of one node
+  const unsigned grid = (unsigned)((n4 / NT + 255) / 256);
   auto launch = [&](int i) {
     const int s = i % nsets;
-    hipLaunchKernelGGL(gather_nt<8>, dim3(grid), dim3(256), 0, st, (const f4*)bufs[3 * s], (f4*)bufs[3 * s + 2], node4,
+    hipLaunchKernelGGL(gather_nt<NT>, dim3(grid), dim3(256), 0, st, (const f4*)bufs[3 * s], (f4*)bufs[3 * s + 2], node4,
                        node4);
   };
   (void)graph_items;
@@ -169,10 +170,11 @@ int main(int argc, char** argv) {
       const double bytes = (double)plane_bytes * (bwd ? 3 : 2);
       printf("%-10s %s %8.1f MB  %8.2f us  %5.1f %% of 8 TB/s  (%d rotating sets)\n", s.name, bwd ? "2r1w" : "1r1w",
              bytes / 1e6, us, bytes / (us * 1e-6) / 8e12 * 100, nsets);
-      if (!bwd && s.N == 8) {  // the forward's gather pattern: 8 node planes per thread, 8 outputs
+      if (!bwd) {  // the forward's gather pattern: N node planes per thread, N outputs
         const size_t node4 = (size_t)s.C * s.HW * s.HW / 4;
-        const double ug = time_gather(nsets, iters, bufs, n4, node4);
-        printf("%-10s gather8 %8.1f MB  %8.2f us  %5.1f %% of 8 TB/s\n", s.name, bytes / 1e6, ug,
+        const double ug = s.N == 8 ? time_gather<8>(nsets, iters, bufs, n4, node4)
+                                   : time_gather<16>(nsets, iters, bufs, n4, node4);
+        printf("%-10s gather%ld %8.1f MB  %8.2f us  %5.1f %% of 8 TB/s\n", s.name, s.N, bytes / 1e6, ug,
                bytes / (ug * 1e-6) / 8e12 * 100);
       }
       fflush(stdout);
