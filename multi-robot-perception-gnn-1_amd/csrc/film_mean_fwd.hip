@@ -90,6 +90,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"bwd_fused_lo", &t.bwd_fused_lo, 1, 256},
       {"bwd_fused_hi", &t.bwd_fused_hi, 1, 256},
       {"bwd_fused_cap", &t.bwd_fused_cap, 1, 64},
+      {"bwd_pre2", &t.bwd_pre2, 0, 1},
       {"bwd_regular_vec", &t.bwd_regular_vec, 1, 2},
       {"bwd_regular_lanes", &t.bwd_regular_lanes, 1, 64},
       {"bwd_regular_slices", &t.bwd_regular_slices, 0, 64},

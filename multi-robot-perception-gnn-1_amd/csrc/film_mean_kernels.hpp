@@ -870,7 +870,11 @@ __device__ __forceinline__ void with_lanes(int lpc, F&& f) {
 //   grad_gb[e, c] = (s_v * D[v][u], s_v * S[v])    for every edge e = (u -> v).
 // For NT > 8 the kernel runs with VB = 4 and loops over destination blocks (x re-read from L2).
 // ---------------------------------------------------------------------------
-template <int NT, int VB, int VEC, bool COMPLETE, bool DXB = false, int MINW = 1>
+// PRE2: lanes own exactly two slices (the launcher checks PV == 2 lpc) and both are loaded before
+// the prologue, into two register sets, so the second slice's loads are in flight while the first
+// is reduced instead of being issued after it.  At N = 8 the kernel runs 2 waves per SIMD either
+// way (192 VGPRs with one set), so the second set costs no occupancy.
+template <int NT, int VB, int VEC, bool COMPLETE, bool DXB = false, int MINW = 1, bool PRE2 = false>
 __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
@@ -913,26 +917,30 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   // weight-tile build (one more round trip to HBM) hides under these loads
   Frag<VEC> gv[VB];
   Frag<VEC> xv[NT];
-  auto load_slice = [&](int vb, int j) {
+  Frag<VEC> gv2[PRE2 ? VB : 1];
+  Frag<VEC> xv2[PRE2 ? NT : 1];
+  auto load_into = [&](Frag<VEC>* G, Frag<VEC>* X, int vb, int j) {
     const uint32_t lane_off = lane_plane + (uint32_t)j * VEC * 4u;
 #pragma unroll
     for (int i = 0; i < VB; ++i) {
       const int v = vb + i;
       const int vv = v < n ? v : n - 1;
-      gv[i] = load_frag<VEC, kOnePass>(at_bytes(gbase + (int64_t)vv * a.gs, lane_off));
+      G[i] = load_frag<VEC, kOnePass>(at_bytes(gbase + (int64_t)vv * a.gs, lane_off));
     }
     if (a.want_dgb) {
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         const int uu = u < n ? u : n - 1;
-        xv[u] = load_frag<VEC, kOnePass>(at_bytes(xbase + (int64_t)uu * a.xs, lane_off));
+        X[u] = load_frag<VEC, kOnePass>(at_bytes(xbase + (int64_t)uu * a.xs, lane_off));
       }
     }
   };
+  auto load_slice = [&](int vb, int j) { load_into(gv, xv, vb, j); };
 
   float2 reg[CompleteSlots<NT>::kPer];
   if (COMPLETE) complete_fetch<NT>(a, (int64_t)b * NT * (NT - 1), c0, 0, reg);
   if (kOnePass && active && li < a.PV) load_slice(0, li);
+  if (PRE2 && active && li < a.PV) load_into(gv2, xv2, 0, li + a.lpc);
   if (COMPLETE) {
     complete_store<NT, true>(a, 0, reg, Wt, nullptr, Sg);
     complete_rest<NT, true>(a, (int64_t)b * NT * (NT - 1), c0, Wt, nullptr, Sg);
@@ -1003,7 +1011,16 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
           }
         }
         j += a.lpc;
-        if (j < a.PV) load_slice(vb, j);
+        if (j < a.PV) {
+          if constexpr (PRE2) {  // the second (last) slice is already in registers
+#pragma unroll
+            for (int i = 0; i < VB; ++i) gv[i] = gv2[i];
+#pragma unroll
+            for (int u = 0; u < NT; ++u) xv[u] = xv2[u];
+          } else {
+            load_slice(vb, j);
+          }
+        }
       }
     }
     if (a.want_dgb) {
@@ -1357,6 +1374,7 @@ struct Tuning {
   // 4x as many, so loads of later workgroups overlap the Gram reduction and epilogue of earlier
   // ones (C=1280 B=32: 60.8 against 67.2 us with 32 channels; 32x32 planes are unaffected: 2)
   int bwd_fused_lo = 8, bwd_fused_hi = 128, bwd_fused_cap = 8;
+  int bwd_pre2 = 1;  // film_bwd_fused: prefetch both slices when a lane owns exactly two
   int bwd_regular_vec = 2, bwd_regular_lanes = 16;              // film_bwd_regular (N > 8, k-NN)
   // film_bwd_regular: split planes so each lane owns this many slices (0: whole planes); needs the
   // caller's workspace (mrp_film_mean_bwd_workspace), else whole planes.  Measured slower at the

@@ -110,6 +110,10 @@ def main():
         for _ in range(3):
             sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0]})
         return
+    if what == "pre2":  # backward with / without the two-slice prefetch
+        for name in ("north_star", "cfg1", "cfg2", "cfg3"):
+            sweep("bwd", name, bwd_time, {"bwd_pre2": [0, 1, 0, 1]})
+        return
     if what == "bwdall":  # the backward at every config shape, default geometry
         for name in ("north_star", "cfg1", "cfg2", "cfg3"):
             sweep("bwd", name, bwd_time, {"bwd_fused_cap": [8]})
