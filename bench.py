@@ -313,7 +313,7 @@ def config_record(cid, world, rank, device, args):
                       "ms_per_step": t * 1e3}
     # which compress path the eval forward took, and the other one for comparison (models.py policy)
     fused = (mrp.models.fused_compress_enabled(P)
-             and mrp.compress.fused_compress_supported(net.conv1, x, csr))
+             and mrp.compress.dual_compress_supported(net.conv1, x))
     prev = mrp.models.fused_compress_setting()
     mrp.models.set_fused_compress(not fused)
     try:
@@ -323,7 +323,8 @@ def config_record(cid, world, rank, device, args):
             t_other = timed(fwd, args.config_steps, world, device, args.dist_backend)
     finally:
         mrp.models.set_fused_compress(prev)
-    rec["forward"]["compress"] = "fused aggregation + MFMA compress kernel" if fused else "cat kernel + library GEMM"
+    rec["forward"]["compress"] = ("aggregate kernel + two-source MFMA compress (no cat buffer)" if fused
+                                  else "cat kernel + library GEMM")
     rec["forward"]["ms_per_step_other_compress"] = t_other * 1e3
     if scaling == "strong":  # every rank holds a different part of one global batch
         tot = torch.tensor([float(elems)], dtype=torch.float64,

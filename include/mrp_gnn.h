@@ -238,6 +238,17 @@ int64_t mrp_film_mean_bwd_workspace(int32_t num_graphs, int32_t max_nodes, int32
  */
 int mrp_compress_weight_pack(const float* w, float* wp, int32_t C, void* stream);
 
+/*
+ * The same compress from an aggregate already in HBM (mrp_film_mean_fwd's output):
+ *   y[v, m, p] = sum_c W[m, c] x[v, c, p] + sum_c W[m, C + c] agg[v, c, p] + bias[m]
+ * for any node count (nodes are tiled in groups of 8; no graph structure involved).  wt packed by
+ * mrp_compress_weight_pack; operands staged by LDS-DMA.  C % 128 == 0, P % 16 == 0, x / agg / wt
+ * 16-byte aligned with node strides multiples of 4 (else hipErrorNotSupported).
+ */
+int mrp_compress_dual_fwd(const float* x, int64_t x_node_stride, const float* agg, int64_t agg_node_stride,
+                          int32_t num_nodes, int32_t C, int32_t P, const float* wt, const float* bias, float* y,
+                          int64_t y_node_stride, void* stream);
+
 int mrp_compress_film_fwd(const float* x, int64_t x_node_stride, const float* gb,
                           int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
                           int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode,
@@ -303,7 +314,8 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 11 = this header: the
- * epilogue entry points of v10 plus mrp_compress_film_fwd, mrp_compress_weight_pack, mrp_film_gate). */
+ * epilogue entry points of v10 plus mrp_compress_film_fwd, mrp_compress_dual_fwd,
+ * mrp_compress_weight_pack, mrp_film_gate). */
 int mrp_abi_version(void);
 
 /* Human-readable text for a return code (static storage). */

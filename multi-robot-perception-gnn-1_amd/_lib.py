@@ -29,6 +29,7 @@ EXPORTED_SYMBOLS = (
     "mrp_compress_film_fwd",
     "mrp_film_gate",
     "mrp_compress_weight_pack",
+    "mrp_compress_dual_fwd",
     "mrp_edge_hidden_fwd",
     "mrp_edge_encoder_bwd_workspace",
     "mrp_edge_encoder_bwd",
@@ -99,6 +100,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_film_gate.restype = ctypes.c_int
     lib.mrp_compress_weight_pack.argtypes = [_P, _P, _I32, _P]
     lib.mrp_compress_weight_pack.restype = ctypes.c_int
+    lib.mrp_compress_dual_fwd.argtypes = [_P, _I64, _P, _I64, _I32, _I32, _I32, _P, _P, _P, _I64, _P]
+    lib.mrp_compress_dual_fwd.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]

@@ -130,3 +130,46 @@ def compress_film_fused(conv: torch.nn.Conv2d, x: torch.Tensor, gb, csr, mode: i
         return None
     _lib.check(code, "mrp_compress_film_fwd")
     return y
+
+
+def dual_compress_supported(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
+    """Whether ``mrp_compress_dual_fwd`` covers this layer (any graph): fp32 CUDA features, a plain
+    1x1 Conv2d(2C, C), C % 128 == 0, H W % 16 == 0."""
+    if x.dim() != 4:
+        return False
+    n, C, H, W = x.shape
+    return (x.is_cuda and x.dtype == torch.float32 and conv.kernel_size == (1, 1) and conv.groups == 1
+            and conv.stride == (1, 1) and conv.dilation == (1, 1) and conv.padding in ((0, 0), "valid")
+            and tuple(conv.weight.shape[:2]) == (C, 2 * C) and conv.weight.dtype == torch.float32
+            and C % 128 == 0 and (H * W) % 16 == 0)
+
+
+def compress_dual(conv: torch.nn.Conv2d, x: torch.Tensor, agg: torch.Tensor):
+    """``conv(torch.cat((x, agg), 1))`` for a 1x1 ``Conv2d(2C, C)`` without the concatenation:
+    ``mrp_compress_dual_fwd`` (fp32 MFMA, operands staged by LDS-DMA).  Forward only.  None when the
+    kernel does not cover the shape (C % 128, H W % 16, alignment)."""
+    n, C, H, W = x.shape
+    if not dual_compress_supported(conv, x) or agg.shape != x.shape or agg.dtype != torch.float32:
+        return None
+    from .aggregate import _ptr, _stream, node_stride
+    xs, gs = node_stride(x), node_stride(agg)
+    if xs is None:
+        x = x.contiguous()
+        xs = C * H * W
+    if gs is None:
+        agg = agg.contiguous()
+        gs = C * H * W
+    wt = _weight_packed(conv)
+    bias = conv.bias.detach() if conv.bias is not None else None
+    if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
+        bias = bias.float().contiguous()
+    y = torch.empty((n, C, H, W), device=x.device, dtype=torch.float32)
+    lib = _lib.load_library()
+    with torch.cuda.device(x.device):
+        code = lib.mrp_compress_dual_fwd(_ptr(x), xs, _ptr(agg), gs, n, C, H * W, _ptr(wt), _ptr(bias), _ptr(y),
+                                         C * H * W, _stream(x.device))
+    if code == _lib.HIP_ERROR_NOT_SUPPORTED:
+        return None
+    _lib.check(code, "mrp_compress_dual_fwd")
+    return y
+

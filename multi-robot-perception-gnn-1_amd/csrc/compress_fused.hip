@@ -125,6 +125,70 @@ struct Lds {
   static constexpr int TOTAL = 2 * BUF;          // double buffer
 };
 
+// One K stage (16 input channels, both halves) of a consumer wave's 32 x (NT x 16) output block:
+// W fragments from the k4-packed image (narrow or wide reads, kWideA), x / aggregate fragments from
+// the [node][channel][pixel] images (kPackB: k4-packed instead).
+template <int NT, int BM>
+__device__ __forceinline__ void consume_stage(f32x4 (&acc)[2][NT], const float* Xs, const float* As, const float* Ws,
+                                              int w, int lk, int lc) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f4* B4 = reinterpret_cast<const f4*>(h == 0 ? Xs : As);
+    const f4* A4 = reinterpret_cast<const f4*>(Ws);
+    f4 af[2], bf[NT];
+    if (kWideA) {
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb) af[mb] = A4[(h * 4 + lk) * BM + 32 * w + 16 * mb + lc];
+    } else {
+      const float* A1 = reinterpret_cast<const float*>(A4);
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) af[mb][k4] = A1[((h * 4 + lk) * BM + 32 * w + 16 * mb + lc) * 4 + k4];
+    }
+    if (kPackB) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bf[j] = B4[(j * 4 + lk) * TP + lc];
+    } else {
+      const float* B1 = reinterpret_cast<const float*>(B4);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) bf[j][k4] = B1[(j * KS + 4 * k4 + lk) * TP + lc];
+    }
+    // k-step k4 covers channels 4 k4 + (0..3) (lane row lk); consecutive MFMAs use different
+    // accumulators, so no dependent issue back to back
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+          acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mb][k4], bf[j][k4], acc[mb][j], 0, 0, 0);
+  }
+}
+
+// Epilogue: D[row = 4 (lane >> 4) + r][col = lane & 15] of block (mb, node j), + bias; nodes past
+// nvalid (a partial node group) are not stored.
+template <int NT, int BM>
+__device__ __forceinline__ void store_tile(const f32x4 (&acc)[2][NT], float* y, int64_t ys, const float* bias, int P,
+                                           int m0, int p0, int64_t node0, int nvalid, int w, int lk, int lc) {
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + 32 * w + 16 * mb + 4 * lk + r;
+      const float bm = bias != nullptr ? bias[m] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        if (j >= nvalid) break;
+        float* yp = y + (node0 + j) * ys + (int64_t)m * P + p0 + lc;
+        __builtin_nontemporal_store(__fadd_rn(acc[mb][j][r], bm), yp);
+      }
+    }
+  }
+}
+
 // Roles (wave-uniform): waves 0..NC-1 are consumers — each owns output rows [32w, 32w + 32) x all N
 // nodes x 16 pixels (2 x N accumulator blocks) and only reads LDS and issues MFMAs; the last 4 waves
 // are producers — producer p fills channels [4p, 4p + 4) of the next stage: x slices of all N nodes,
@@ -367,57 +431,102 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
     const float* As = Xs + L::XS;
     const float* Ws = As + L::XS;
     if (a.debug & 2) continue;  // lab: producers only
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f4* B4 = reinterpret_cast<const f4*>(h == 0 ? Xs : As);
-      const f4* A4 = reinterpret_cast<const f4*>(Ws);
-      f4 af[2], bf[NT];
-      if (kWideA) {
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) af[mb] = A4[(h * 4 + lk) * BM + 32 * w + 16 * mb + lc];
-      } else {
-        const float* A1 = reinterpret_cast<const float*>(A4);
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-          for (int k4 = 0; k4 < 4; ++k4) af[mb][k4] = A1[((h * 4 + lk) * BM + 32 * w + 16 * mb + lc) * 4 + k4];
-      }
-      if (kPackB) {
-#pragma unroll
-        for (int j = 0; j < NT; ++j) bf[j] = B4[(j * 4 + lk) * TP + lc];
-      } else {
-        const float* B1 = reinterpret_cast<const float*>(B4);
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-          for (int k4 = 0; k4 < 4; ++k4) bf[j][k4] = B1[(j * KS + 4 * k4 + lk) * TP + lc];
-      }
-      // k-step k4 covers channels 4 k4 + (0..3) (lane row lk); consecutive MFMAs use different
-      // accumulators, so no dependent issue back to back
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4)
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-          for (int mb = 0; mb < 2; ++mb)
-            acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mb][k4], bf[j][k4], acc[mb][j], 0, 0, 0);
-    }
+    consume_stage<NT, BM>(acc, Xs, As, Ws, w, lk, lc);
   }
 
-  // epilogue: D[row = 4 (lane >> 4) + r][col = lane & 15] of block (mb, node j), + bias
+  store_tile<NT, BM>(acc, a.y, a.ys, a.bias, a.P, m0, p0, node0, NT, w, lk, lc);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two-source form: y = W[:, :C] x + W[:, C:] agg + b with agg already in HBM (mrp_film_mean_fwd's
+// output), i.e. the compress of models.py:181-184 without the (N, 2C, P) concatenation.  Same tiles
+// and consumer waves as the fused kernel; the producers only move operands, by LDS-DMA
+// (global_load_lds_dwordx4: no VGPRs, no VALU, 1 KiB per instruction) — 32 per stage per
+// workgroup, 8 per producer wave: x of 8 nodes, agg of 8 nodes, the W stage's 16 KiB.  One stage
+// ahead: stage s+1 is issued right after barrier #s (its buffer was consumed before that barrier)
+// and retired by the vmcnt(0) __syncthreads emits at barrier #(s+1).  Nodes are taken in groups of 8
+// (any node count: a partial last group re-loads its last node and stores only its own nodes).
+// ---------------------------------------------------------------------------------------------
+struct DualArgs {
+  const float* x;
+  int64_t xs;
+  const float* g;  // aggregate
+  int64_t gs;
+  const float* wt;  // packed weight (mrp_compress_weight_pack)
+  const float* bias;
+  float* y;
+  int64_t ys;
+  int32_t C, P, num_nodes, ntiles_p, ntiles_m, remap;
+};
+
+__global__ void __launch_bounds__(Geo<4>::THREADS) compress_dual_fwd(DualArgs a) {
+  constexpr int NT = 8, NC = 4;
+  using L = Lds<NT, NC>;
+  constexpr int BM = Geo<NC>::BM;
+  extern __shared__ f4 smem_f4[];
+  float* smem = reinterpret_cast<float*>(smem_f4);
+  int id = blockIdx.x;
+  if (a.remap) id = (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+  const int mt = id % a.ntiles_m;
+  const int rest = id / a.ntiles_m;
+  const int pt = rest % a.ntiles_p;
+  const int grp = rest / a.ntiles_p;
+  const int m0 = mt * BM, p0 = pt * TP;
+  const int64_t node0 = (int64_t)grp * NT;
+  const int nvalid = (int)min((int64_t)NT, (int64_t)a.num_nodes - node0);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nstages = a.C / KS;
+
+  if (w >= NC) {
+    const int pw = w - NC;  // 0: x, 1: agg, 2 / 3: W halves 0 / 1
+    const int r = lane >> 2, q = lane & 3;  // x / agg: channel row within the stage, 16-byte chunk
+    // LDS destinations as float4 indices into the __shared__ array itself (the builtin needs an
+    // LDS-typed pointer; the wave's 64 lanes land at dst + lane)
+    auto issue = [&](int s) {
+      const int buf4 = (s & 1) * L::BUF / 4;
+      const int c0 = s * KS;
+      if (pw < 2) {
+        const float* src = pw == 0 ? a.x : a.g;
+        const int64_t ss = pw == 0 ? a.xs : a.gs;
+        const int dst4 = buf4 + pw * L::XS / 4;
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb) {
+        for (int u = 0; u < NT; ++u) {
+          const int64_t node = node0 + min(u, nvalid - 1);
+          const float* gp = src + node * ss + (int64_t)(c0 + r) * a.P + p0 + 4 * q;
+          __builtin_amdgcn_global_load_lds(gp, &smem_f4[dst4 + u * KS * TP / 4], 16, 0, 0);
+        }
+      } else {
+        const int h = pw - 2;
+        const int dst4 = buf4 + 2 * L::XS / 4;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + 32 * w + 16 * mb + 4 * lk + r;
-      const float bm = a.bias != nullptr ? a.bias[m] : 0.f;
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        float* yp = a.y + (int64_t)(node0 + j) * a.ys + (int64_t)m * a.P + p0 + lc;
-        __builtin_nontemporal_store(__fadd_rn(acc[mb][j][r], bm), yp);
+        for (int i = 0; i < 8; ++i) {  // (lk, half) of this W half: 2 KiB per lk
+          const int lk = i >> 1, half = i & 1;
+          const float* gp = a.wt + ((((int64_t)h * (a.C / KS) + s) * 4 + lk) * a.C + m0 + 64 * half + lane) * 4;
+          __builtin_amdgcn_global_load_lds(gp, &smem_f4[dst4 + (h * 4 + lk) * BM + 64 * half], 16, 0, 0);
+        }
       }
+    };
+    issue(0);
+    for (int s = 0; s < nstages; ++s) {
+      __syncthreads();  // barrier #s: stage s landed (vmcnt(0)); stage s-1's buffer is free
+      if (s + 1 < nstages) issue(s + 1);
     }
+    return;
   }
+
+  f32x4 acc[2][NT];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[mb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int lk = lane >> 4, lc = lane & 15;
+  for (int s = 0; s < nstages; ++s) {
+    __syncthreads();
+    const float* Xs = smem + (s & 1) * L::BUF;
+    consume_stage<NT, BM>(acc, Xs, Xs + L::XS, Xs + 2 * L::XS, w, lk, lc);
+  }
+  store_tile<NT, BM>(acc, a.y, a.ys, a.bias, a.P, m0, p0, node0, nvalid, w, lk, lc);
 }
 
 // gamma/beta = sigmoid(z), the aggregation kernels' own expression (fast_math.hpp):
@@ -513,6 +622,46 @@ extern "C" int mrp_film_gate(const float* z, float* gb, int64_t n, void* stream)
 // kernel-lab hook (tools/exp_compress_fused.py): not part of the ABI header
 extern "C" void mrp_compress_film_debug(int mode) { mrp_cf_debug = mode; }
 extern "C" void mrp_compress_film_debug_stamps(long long* device_buffer) { mrp_cf_stamps = device_buffer; }
+
+extern "C" int mrp_compress_dual_fwd(const float* x, int64_t x_node_stride, const float* agg, int64_t agg_node_stride,
+                                     int32_t num_nodes, int32_t C, int32_t P, const float* wt, const float* bias, float* y,
+                                     int64_t y_node_stride, void* stream) {
+  if (num_nodes < 0 || C < 0 || P < 0) return hipErrorInvalidValue;
+  if (C % 128 != 0 || P % mrp_cf::TP != 0 || C == 0) return hipErrorNotSupported;
+  if (num_nodes == 0 || P == 0) return hipSuccess;
+  const int64_t plane = (int64_t)C * P;
+  if (!x || !agg || !y || !wt || x_node_stride < plane || agg_node_stride < plane || y_node_stride < plane)
+    return hipErrorInvalidValue;
+  // 16-byte LDS-DMA pieces: every row start 16-byte aligned
+  if ((reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(agg) & 15) ||
+      (reinterpret_cast<uintptr_t>(wt) & 15) || (x_node_stride & 3) || (agg_node_stride & 3) || (P & 3))
+    return hipErrorNotSupported;
+  mrp_cf::DualArgs a;
+  a.x = x;
+  a.xs = x_node_stride;
+  a.g = agg;
+  a.gs = agg_node_stride;
+  a.wt = wt;
+  a.bias = bias;
+  a.y = y;
+  a.ys = y_node_stride;
+  a.C = C;
+  a.P = P;
+  a.num_nodes = num_nodes;
+  a.ntiles_p = P / mrp_cf::TP;
+  a.ntiles_m = C / mrp_cf::Geo<4>::BM;
+  const int64_t groups = ((int64_t)num_nodes + 7) / 8;
+  const int64_t grid = groups * a.ntiles_p * a.ntiles_m;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  a.remap = grid % 8 == 0 ? 1 : 0;
+  const size_t lds = (size_t)mrp_cf::Lds<8, 4>::TOTAL * sizeof(float);
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&mrp_cf::compress_dual_fwd),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(mrp_cf::compress_dual_fwd, dim3((unsigned)grid), dim3(mrp_cf::Geo<4>::THREADS), lds,
+                     static_cast<hipStream_t>(stream), a);
+  return hipGetLastError();
+}
 
 extern "C" int mrp_compress_film_fwd(const float* x, int64_t x_node_stride, const float* gb, int32_t num_graphs,
                                      int32_t max_nodes, int32_t graph_kind, int32_t num_nodes, int32_t num_edges,

@@ -34,7 +34,8 @@ import torch
 import torch.nn as nn
 
 from .aggregate import film_mean, film_mean_cat, film_mean_mix, film_mean_residual
-from .compress import compress_1x1, compress_film_fused, fused_compress_supported
+from .compress import (compress_1x1, compress_dual, compress_film_fused, dual_compress_supported,
+                       fused_compress_supported)
 from .encoder import edge_logits
 
 
@@ -131,19 +132,26 @@ class GCN(nn.Module):
 
     def forward_cat_compress(self, g, feats: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
         """``conv(torch.cat((feats, self(g, feats)), 1))`` (``models.py:181-184``).  Without autograd
-        (eval, ``test_dgl``) the aggregation runs inside the compress GEMM's operand producer
-        (``mrp_compress_film_fwd``: one kernel, no concatenation buffer) where that kernel covers the
-        shape; otherwise the cat kernel + batched GEMM."""
+        (eval, ``test_dgl``), on the planes where it measured faster (``set_fused_compress``), the
+        concatenation is never written: the aggregate kernel, then the two-source MFMA compress
+        (``mrp_compress_dual_fwd``), or the single fused kernel (``mrp_compress_film_fwd``) in
+        "fused" mode; otherwise (and with autograd) the cat kernel + batched GEMM."""
         x = feats
+        setting = fused_compress_setting()
         if (x.is_cuda and self._return_mode() != "input" and not torch.is_grad_enabled()
-                and _opt(self.opt, "gcn_mode", "film_mean") != "copy_mean"
-                and fused_compress_enabled(x.shape[-2] * x.shape[-1])
-                and fused_compress_supported(conv, x, g.csr(x.device))):
-            mode = _lib_modes()[_opt(self.opt, "gcn_mode", "film_mean")]
-            z = self.edge_encoder.logits(g.edata["pose"])
-            y = compress_film_fused(conv, x, z, g.csr(x.device), mode | _lib_logits())
-            if y is not None:
-                return y
+                and fused_compress_enabled(x.shape[-2] * x.shape[-1])):
+            if setting == "fused":
+                if (_opt(self.opt, "gcn_mode", "film_mean") != "copy_mean"
+                        and fused_compress_supported(conv, x, g.csr(x.device))):
+                    mode = _lib_modes()[_opt(self.opt, "gcn_mode", "film_mean")]
+                    z = self.edge_encoder.logits(g.edata["pose"])
+                    y = compress_film_fused(conv, x, z, g.csr(x.device), mode | _lib_logits())
+                    if y is not None:
+                        return y
+            elif dual_compress_supported(conv, x):
+                y = compress_dual(conv, x, self(g, x))
+                if y is not None:
+                    return y
         return compress_1x1(conv, self.forward_cat(g, x))
 
     def forward_residual(self, g, feats: torch.Tensor = None) -> torch.Tensor:
@@ -172,9 +180,10 @@ class GCN(nn.Module):
 
 
 _FUSED_COMPRESS = ["auto"]
-# "auto": the fused kernel where it measured faster than cat kernel + library GEMM (DESIGN.md,
-# fused compress): large planes (configs[1], 32x32: 1.18 ms vs 1.25 ms per layer); on 8x8 planes
-# (configs[2]/[3]) the 4 pixel tiles per graph leave the grid short and the unfused path wins
+# "auto": the concatenation-free compress where it measured faster than cat kernel + library GEMM
+# (DESIGN.md §3.6): planes of >= 256 pixels (configs[1], 32x32: aggregate 90 us + two-source GEMM
+# 1.02 ms = 1.11 ms vs 1.23 ms per layer; configs[4] 16x16); on 8x8 planes (configs[2]/[3]) the
+# library GEMM on the cat buffer is 3-4 % faster and stays
 FUSED_MIN_PLANE = 256
 
 
@@ -190,9 +199,10 @@ def fused_compress_setting():
 
 
 def set_fused_compress(enabled) -> None:
-    """The fused aggregation + compress kernel (inference path): True (wherever the kernel covers the
-    shape), False (never) or "auto" (default: where it measured faster)."""
-    _FUSED_COMPRESS[0] = "auto" if enabled == "auto" else bool(enabled)
+    """The concatenation-free compress of the inference path: True (aggregate kernel + two-source
+    MFMA GEMM wherever it covers the shape), "fused" (the single fused kernel instead), False (cat
+    kernel + library GEMM) or "auto" (default: the two-source path where it measured faster)."""
+    _FUSED_COMPRESS[0] = enabled if enabled in ("auto", "fused") else bool(enabled)
 
 
 def _lib_modes():

@@ -131,3 +131,60 @@ def test_weight_pack_layout(cuda_device, C):
     with torch.no_grad():
         conv.weight.mul_(2)
     assert torch.equal(_weight_packed(conv).cpu(), ref * 2)
+
+
+@pytest.mark.parametrize("n,C,H", [(128, 512, 8), (37, 128, 4), (8, 256, 16), (5, 384, 4)])
+def test_dual_compress(cuda_device, n, C, H):
+    """mrp_compress_dual_fwd: conv(cat(x, agg)) from two sources, any node count (partial last
+    group of 8).  Selector weights make it exact; random weights within the GEMM yardstick."""
+    from mrp_gnn_amd.compress import compress_dual
+    torch.manual_seed(n + C)
+    x = torch.randn(n, C, H, H, device=cuda_device)
+    agg = torch.randn(n, C, H, H, device=cuda_device)
+    eye, zero = torch.eye(C), torch.zeros(C, C)
+    y = compress_dual(conv_with(C, torch.cat((zero, eye), 1)).to(cuda_device), x, agg)
+    assert y is not None and torch.equal(y, agg)
+    y = compress_dual(conv_with(C, torch.cat((eye, zero), 1)).to(cuda_device), x, agg)
+    assert torch.equal(y, x)
+    conv = torch.nn.Conv2d(2 * C, C, 1).to(cuda_device)
+    y = compress_dual(conv, x, agg)
+    w, b = conv.weight.detach(), conv.bias.detach()
+    ok, e = stack_ref.within(y, stack_ref.conv1x1(torch.cat((x, agg), 1), w, b),
+                             stack_ref.conv1x1(torch.cat((x, agg), 1).double(), w.double(), b.double()))
+    assert ok, e
+
+
+def test_dual_equals_fused(cuda_device):
+    """The two-pass path (aggregate kernel, then the dual GEMM) gives the fused kernel's bits: the same
+    aggregate and the same MFMA K order."""
+    from mrp_gnn_amd.compress import compress_dual
+    g = frames(4, 8, 256, 8, seed=11).to(cuda_device)
+    x = g.ndata["image"]
+    z = torch.randn(g.num_edges(), 256, 2, device=cuda_device)
+    csr = g.csr(cuda_device)
+    conv = torch.nn.Conv2d(512, 256, 1).to(cuda_device)
+    mode = m._lib.MODE_FILM_MEAN | m._lib.GB_LOGITS
+    fused = compress_film_fused(conv, x, z, csr, mode)
+    agg = m.film_mean(x, z, csr, logits=True)
+    assert torch.equal(compress_dual(conv, x, agg), fused)
+
+
+def test_stack_eval_fused_mode(cuda_device):
+    """set_fused_compress("fused"): the single fused kernel in the eval stack, equal to the two-pass
+    path bit for bit (same aggregate, same MFMA order)."""
+    C = 256
+    opt = types.SimpleNamespace(feature_dim=C, compress_gcn=True, multi_gcn=True)
+    torch.manual_seed(1)
+    net = m.GCNBlock(opt).to(cuda_device)
+    g = frames(3, 8, C, 8, seed=4).to(cuda_device)
+    x = g.ndata["image"]
+    prev = m.models.fused_compress_setting()
+    try:
+        with torch.no_grad():
+            m.models.set_fused_compress("fused")
+            a = net(g, x)
+            m.models.set_fused_compress(True)
+            b = net(g, x)
+    finally:
+        m.models.set_fused_compress(prev)
+    assert torch.equal(a, b)

@@ -8,7 +8,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import mrp_gnn_amd as mrp  # noqa: E402
 from bench import make_workload, time_launches  # noqa: E402
-from mrp_gnn_amd.compress import compress_1x1, compress_film_fused  # noqa: E402
+from mrp_gnn_amd.compress import compress_1x1, compress_dual, compress_film_fused  # noqa: E402
 
 dev = torch.device("cuda:0")
 MODE = mrp._lib.MODE_FILM_MEAN | mrp._lib.GB_LOGITS
@@ -26,8 +26,13 @@ for name, (B, N, C, H) in {"cfg1": (16, 8, 512, 32), "cfg2": (32, 8, 1280, 8), "
         cat = torch.empty(x.shape[0], 2 * C, H, H, device=dev)
         t_cat = time_launches([lambda: mrp.film_mean_cat_forward_into(x, z, csr, MODE, cat)], 20, dev)
         t_gemm = time_launches([lambda: compress_1x1(conv, cat)], 20, dev)
-        t_fused = time_launches([lambda: compress_film_fused(conv, x, z, csr, MODE)], 20, dev)
         flop = 2 * x.shape[0] * H * H * C * 2 * C
+        t_fused = time_launches([lambda: compress_film_fused(conv, x, z, csr, MODE)], 20, dev)
+        agg = torch.empty_like(x)
+        t_agg = time_launches([lambda: mrp.film_mean_forward_into(x, z, csr, MODE, agg)], 20, dev)
+        t_dual = time_launches([lambda: compress_dual(conv, x, agg)], 20, dev)
+        print(f"{name}: two-pass: aggregate {t_agg * 1e6:8.1f} us + dual GEMM {t_dual * 1e6:8.1f} us "
+              f"({flop / t_dual / 1e12:6.1f} TF/s) = {(t_agg + t_dual) * 1e6:8.1f} us", flush=True)
         lab = []
         for mode in (1, 2):  # 1: consumers only (MFMA bound), 2: producers only
             lib.mrp_compress_film_debug(mode)
