@@ -444,7 +444,7 @@ __global__ void __launch_bounds__(Geo<NC>::THREADS) compress_film_fwd(Args a) {
 // (global_load_lds_dwordx4: no VGPRs, no VALU, 1 KiB per instruction) — 32 per stage per
 // workgroup, 8 per producer wave: x of 8 nodes, agg of 8 nodes, the W stage's 16 KiB.  One stage
 // ahead: stage s+1 is issued right after barrier #s (its buffer was consumed before that barrier)
-// and retired by the vmcnt(0) __syncthreads emits at barrier #(s+1).  Nodes are taken in groups of 8
+// and retired by the producers' explicit vmcnt(0) ahead of barrier #(s+1).  Nodes are taken in groups of 8
 // (any node count: a partial last group re-loads its last node and stores only its own nodes).
 // ---------------------------------------------------------------------------------------------
 struct DualArgs {
@@ -509,7 +509,11 @@ __global__ void __launch_bounds__(Geo<4>::THREADS) compress_dual_fwd(DualArgs a)
     };
     issue(0);
     for (int s = 0; s < nstages; ++s) {
-      __syncthreads();  // barrier #s: stage s landed (vmcnt(0)); stage s-1's buffer is free
+      // LDS-DMA writes are tracked by the issuing wave's vmcnt only: the compiler's workgroup fence
+      // waits for LDS (lgkmcnt) but not for them, so without this wait the consumers could read a
+      // stage that has not landed (tools/exp_determinism.py caught it: NaN / run-to-run differences)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // barrier #s: stage s landed; stage s-1's buffer is free
       if (s + 1 < nstages) issue(s + 1);
     }
     return;

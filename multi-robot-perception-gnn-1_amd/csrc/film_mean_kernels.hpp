@@ -589,7 +589,8 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
 // wave-uniform dynamic index into the slice registers (lowered to M0-relative moves, no scratch).
 // Summation order = slot order, as the mailbox mean: acc = fl(acc + fl(fl(gamma x_u) + beta)),
 // out = fl(acc / K).  Like film_fwd with COMPLETE graphs, the plane may be split over psplit
-// workgroups (the prologue is two rounds of loads: CSR slots, then gamma/beta).
+// workgroups (the prologue is two rounds of loads: edge ids, then gamma/beta, both in flight
+// together with the first slice).
 // ---------------------------------------------------------------------------
 template <int NT, int KMAX, int VEC>
 __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
@@ -600,7 +601,6 @@ __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
   extern __shared__ float4 smem_f4[];
   float2* Wl = reinterpret_cast<float2*>(smem_f4);                  // [cpb][WS] (gamma, beta) per slot
   unsigned* slot_u = reinterpret_cast<unsigned*>(Wl + a.cpb * WS);  // [NT * WPD] packed local sources
-  int* slot_e = reinterpret_cast<int*>(slot_u + NT * WPD);          // [NS] edge id of the slot (-1: none)
 
   const int ps = a.psplit > 1 ? a.psplit : 1;
   const int item = blockIdx.x / ps;
@@ -640,44 +640,75 @@ __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
       for (int k = 0; k < VEC; ++k) xs[k][u] = f.v[k];
     }
   };
-  if (active && j < jend) load_slice(j);
 
-  // prologue 1: the graph's slots (channel-independent)
-  for (int t = threadIdx.x; t < NT * WPD; t += blockDim.x) {
-    const int v = t / WPD, q = t - v * WPD;
-    unsigned word = 0u;
+  // Prologue.  Loads retire in issue order (vmcnt), so whatever the prologue waits for must be
+  // issued before the first slice's loads, or waiting for it waits for the slices too.  Order:
+  // slot sources and edge ids -> first slice -> gamma/beta (need only the edge ids) -> LDS, one
+  // barrier.  Every thread fetches the edge ids of its own (channel, slot) items (v's CSR row is
+  // [K v, K (v+1)) for REGULAR graphs, so no indptr), so no barrier sits between the two rounds.
+  constexpr int IPT = 2;  // (channel, slot) items per thread fetched ahead of the slice (the rest after)
+  const int nitem = a.cpb * NS;
+  const bool film = a.mode != MRP_AGG_COPY_MEAN;
+  auto slot_eid = [&](int t, int& cl, int& slot) -> int {
+    split_channel(a, t, cl, slot);  // channel fastest: neighbouring lanes read neighbouring pairs
+    const int v = slot / KMAX, jj = slot - v * KMAX;
+    if (t >= nitem || v >= n || jj >= K || c0 + cl >= a.C) return -1;
+    return a.eid[(node0 + v) * K + jj];
+  };
+  auto fetch_w = [&](int e, int cl) -> float2 {
+    if (e < 0) return make_float2(0.f, 0.f);     // empty slot: multiply by 0, add 0
+    if (!film) return make_float2(1.f, 0.f);     // gamma 1, beta 0: fl(fl(1*x) + 0) = x
+    return *reinterpret_cast<const float2*>(a.gb + ((int64_t)e * a.C + c0 + cl) * 2);
+  };
+  auto store_w = [&](float2 w, int e, int cl, int slot) {
+    if (e >= 0 && film && a.logits) w = make_float2(sigmoidf(w.x), sigmoidf(w.y));
+    Wl[cl * WS + slot] = w;
+  };
+  // the graph's slot sources (channel-independent), WPD words of four 8-bit sources per destination
+  const bool has_word = threadIdx.x < NT * WPD;
+  int srcs[4];
+  if (has_word) {
+    const int v = threadIdx.x / WPD, q = threadIdx.x - v * WPD;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int jj = q * 4 + i;
-      int u = 0, e = -1;
-      if (v < n && jj < K) {
-        const int k = (node0 + v) * K + jj;  // REGULAR: v's CSR row is [K*v, K*(v+1))
-        u = a.src[k] - node0;
-        e = a.eid[k];
-        if ((unsigned)u >= (unsigned)n) { u = 0; e = -1; }  // leaves the graph: rejected on the host
-      }
-      word |= (unsigned)u << (8 * i);
-      slot_e[v * KMAX + jj] = e;
+      srcs[i] = v < n && jj < K ? a.src[(node0 + v) * K + jj] - node0 : 0;
     }
-    slot_u[t] = word;
   }
-  __syncthreads();
-  // prologue 2: (gamma, beta) of every (channel, slot); an empty slot multiplies by 0 and adds 0
-  for (int t = threadIdx.x; t < a.cpb * NS; t += blockDim.x) {
-    int cl, slot;  // channel fastest: neighbouring lanes read neighbouring gamma/beta pairs
-    split_channel(a, t, cl, slot);
-    const int cc = c0 + cl;
-    const int e = slot_e[slot];
-    float2 w = make_float2(0.f, 0.f);
-    if (e >= 0 && cc < a.C) {
-      if (a.mode == MRP_AGG_COPY_MEAN) {
-        w = make_float2(1.f, 0.f);  // gamma 1, beta 0: fl(fl(1*x) + 0) = x
-      } else {
-        w = *reinterpret_cast<const float2*>(a.gb + ((int64_t)e * a.C + cc) * 2);
-        if (a.logits) w = make_float2(sigmoidf(w.x), sigmoidf(w.y));
-      }
+  int ie[IPT];  // (channel, slot) of an item are recomputed below rather than held across the slice
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    int cl, slot;
+    ie[i] = slot_eid(threadIdx.x + i * blockDim.x, cl, slot);
+  }
+  if (active && j < jend) load_slice(j);
+  float2 iw[IPT];
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    int cl, slot;
+    split_channel(a, threadIdx.x + i * blockDim.x, cl, slot);
+    iw[i] = fetch_w(ie[i], cl);
+  }
+  if (has_word) {
+    unsigned word = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // a source outside the graph is rejected on the host; clamp it anyway (in-bounds register index)
+      const int u = (unsigned)srcs[i] < (unsigned)n ? srcs[i] : 0;
+      word |= (unsigned)u << (8 * i);
     }
-    Wl[cl * WS + slot] = w;
+    slot_u[threadIdx.x] = word;
+  }
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    int cl, slot;
+    split_channel(a, threadIdx.x + i * blockDim.x, cl, slot);
+    if (threadIdx.x + i * blockDim.x < nitem) store_w(iw[i], ie[i], cl, slot);
+  }
+  for (int t = threadIdx.x + IPT * blockDim.x; t < nitem; t += blockDim.x) {  // narrow workgroups only
+    int cl, slot;
+    const int e = slot_eid(t, cl, slot);
+    store_w(fetch_w(e, cl), e, cl, slot);
   }
   __syncthreads();
   if (!active) return;
@@ -1186,21 +1217,85 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
     }
   };
   int j = jbeg + li;
-  if (active && j < jend) load_slice(j);
 
-  for (int t = threadIdx.x; t < NS; t += blockDim.x) {
-    const int v = t / KMAX, j = t - v * KMAX;
-    int u = 0, e = -1;
-    const int k = v < n ? a.indptr[node0 + v] + j : 0;
-    if (v < n && j < K && k < a.indptr[node0 + v + 1]) {  // the host checked the degrees; stay in bounds anyway
-      u = a.src[k] - node0;
-      e = a.eid[k];
-      if ((unsigned)u >= (unsigned)n) { u = 0; e = -1; }  // leaves the graph: rejected on the host
+  // Prologue: one (channel, destination v) item per thread builds column v of the channel's
+  // transposed tile, Wt[u][v] = s_v * sum of gamma over v's slots with source u (CSR order, as the
+  // CSR builder), and for channel 0 the slot table.  v's CSR row is [K v, K (v+1)) (REGULAR), so the
+  // sources and edge ids are one round of loads, issued before the first slice's loads (vmcnt
+  // retires in order: waiting for them must not wait for the slices); gamma follows the slice.
+  // Every column entry is written, so no zero-fill pass and a single barrier.
+  constexpr int IPT = 2;  // items per thread fetched ahead of the slice (the rest, narrow workgroups, after)
+  const int nitem = a.cpb * NT;
+  float s = a.mode != MRP_AGG_FILM_SUM && K > 0 ? 1.f / (float)K : 1.f;
+  s *= a.agg_scale;  // epilogue: grad_out reaches the aggregate scaled
+  struct Item {
+    int cl, v;
+    bool ok;
+    int u[KMAX], e[KMAX];
+    float gam[KMAX];
+  };
+  auto item_ids = [&](int t, Item& it) {
+    split_channel(a, t, it.cl, it.v);  // channel fastest: neighbouring lanes read neighbouring pairs
+    it.ok = t < nitem && it.v < n && c0 + it.cl < a.C;
+#pragma unroll
+    for (int jj = 0; jj < KMAX; ++jj) {
+      const bool on = it.ok && jj < K;
+      const int k = (node0 + (on ? it.v : 0)) * K + (on ? jj : 0);
+      it.u[jj] = on ? a.src[k] - node0 : -1;
+      it.e[jj] = on ? a.eid[k] : -1;
     }
-    slot_u[t] = u;
-    slot_e[t] = e;
+  };
+  auto item_gamma = [&](Item& it) {
+#pragma unroll
+    for (int jj = 0; jj < KMAX; ++jj) {
+      float gm = 0.f;
+      if (it.e[jj] >= 0) {
+        if (a.mode == MRP_AGG_COPY_MEAN) {
+          gm = 1.f;
+        } else {
+          gm = a.gb[((int64_t)it.e[jj] * a.C + c0 + it.cl) * 2];
+          if (a.logits) gm = sigmoidf(gm);
+        }
+      }
+      it.gam[jj] = gm;
+    }
+  };
+  auto item_store = [&](int t, const Item& it) {
+    if (t >= nitem) return;
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      float w = 0.f;  // += in slot order: multi-edges sum like the CSR tile build
+#pragma unroll
+      for (int jj = 0; jj < KMAX; ++jj)
+        if (it.u[jj] == u) w += s * it.gam[jj];
+      Wt[it.cl * SZ + u * NTP + it.v] = w;
+    }
+    if (it.cl == 0) {
+      sc[it.v] = it.ok ? s : 0.f;
+#pragma unroll
+      for (int jj = 0; jj < KMAX; ++jj) {
+        // a source outside the graph is rejected on the host; keep the slot harmless anyway
+        const bool in = (unsigned)it.u[jj] < (unsigned)n;
+        slot_u[it.v * KMAX + jj] = in ? it.u[jj] : 0;
+        slot_e[it.v * KMAX + jj] = in ? it.e[jj] : -1;
+      }
+    }
+  };
+  Item items[IPT];
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) item_ids(threadIdx.x + i * blockDim.x, items[i]);
+  if (active && j < jend) load_slice(j);
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    item_gamma(items[i]);
+    item_store(threadIdx.x + i * blockDim.x, items[i]);
   }
-  build_tiles_csr<NT, true>(a, node0, n, c0, Wt, nullptr, sc, nullptr);
+  for (int t = threadIdx.x + IPT * blockDim.x; t < nitem; t += blockDim.x) {
+    Item it;
+    item_ids(t, it);
+    item_gamma(it);
+    item_store(t, it);
+  }
   __syncthreads();
 
   float D[NS];
@@ -1417,8 +1512,7 @@ size_t lds_fwd(int cpb) {
 }
 template <int NT, int KMAX>
 size_t lds_fwd_regular(int cpb) {
-  return (size_t)cpb * (NT * KMAX + 2) * sizeof(float2) + (size_t)NT * (KMAX / 4) * sizeof(unsigned) +
-         (size_t)NT * KMAX * sizeof(int);
+  return (size_t)cpb * (NT * KMAX + 2) * sizeof(float2) + (size_t)NT * (KMAX / 4) * sizeof(unsigned);
 }
 template <int NT>
 size_t lds_dx(int cpb) {

@@ -181,10 +181,10 @@ class GCN(nn.Module):
 
 _FUSED_COMPRESS = ["auto"]
 # "auto": the concatenation-free compress where it measured faster than cat kernel + library GEMM
-# (DESIGN.md §3.6): planes of >= 256 pixels (configs[1], 32x32: aggregate 90 us + two-source GEMM
-# 1.02 ms = 1.11 ms vs 1.23 ms per layer; configs[4] 16x16); on 8x8 planes (configs[2]/[3]) the
-# library GEMM on the cat buffer is 3-4 % faster and stays
-FUSED_MIN_PLANE = 256
+# (DESIGN.md §3.6): planes of >= 1024 pixels (configs[1], 32x32: aggregate 92 us + two-source GEMM
+# 1.05 ms = 1.14 ms vs 1.24 ms per layer); at 16x16 (configs[4]) the two tie (1.09 vs 1.07 ms) and on
+# 8x8 planes (configs[2]/[3]) the library GEMM on the cat buffer is 4-7 % faster, so those stay
+FUSED_MIN_PLANE = 1024
 
 
 def fused_compress_enabled(plane: int = None) -> bool:

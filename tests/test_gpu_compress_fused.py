@@ -169,6 +169,24 @@ def test_dual_equals_fused(cuda_device):
     assert torch.equal(compress_dual(conv, x, agg), fused)
 
 
+def test_dual_equals_fused_configs1_size_repeated(cuda_device):
+    """configs[1]'s shape (B=16, N=8, C=512, 32x32: 4096 workgroups in flight), five launches: every
+    launch gives the fused kernel's bits.  A stage read before its LDS-DMA landed (the producers'
+    vmcnt wait) shows up here as NaN or run-to-run differences; small grids hid it."""
+    from mrp_gnn_amd.compress import compress_dual
+    g = frames(16, 8, 512, 32, seed=12).to(cuda_device)
+    x = g.ndata["image"]
+    z = torch.randn(g.num_edges(), 512, 2, device=cuda_device)
+    csr = g.csr(cuda_device)
+    conv = torch.nn.Conv2d(1024, 512, 1).to(cuda_device)
+    mode = m._lib.MODE_FILM_MEAN | m._lib.GB_LOGITS
+    fused = compress_film_fused(conv, x, z, csr, mode)
+    assert torch.isfinite(fused).all()
+    agg = m.film_mean(x, z, csr, logits=True)
+    for _ in range(5):
+        assert torch.equal(compress_dual(conv, x, agg), fused)
+
+
 def test_stack_eval_fused_mode(cuda_device):
     """set_fused_compress("fused"): the single fused kernel in the eval stack, equal to the two-pass
     path bit for bit (same aggregate, same MFMA order)."""

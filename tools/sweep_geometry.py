@@ -110,6 +110,11 @@ def main():
         for _ in range(3):
             sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0]})
         return
+    if what == "cfg4":  # repeated k-NN forward and backward timings
+        for _ in range(3):
+            sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0]})
+            sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [2]})
+        return
     if what == "pre2":  # backward with / without the two-slice prefetch
         for name in ("north_star", "cfg1", "cfg2", "cfg3"):
             sweep("bwd", name, bwd_time, {"bwd_pre2": [0, 1, 0, 1]})
