@@ -11,6 +11,13 @@ namespace {
 template <int NT, int KMAX>
 hipError_t launch_fwd_regular(const AggArgs& a, const Geometry& g, hipStream_t st) {
   const size_t lds = lds_fwd_regular<NT, KMAX>(g.cpb);
+  // k-NN(4) in a mean mode (BASELINE configs[4]): compile-time degree, exact division by 4
+  if constexpr (KMAX == 4) {
+    if (g.vec == 4 && a.kdeg == 4 && a.mode != MRP_AGG_FILM_SUM) {
+      MRP_LAUNCH((mrp::film_fwd_regular<NT, KMAX, 4, 4>), lds);
+      return hipGetLastError();
+    }
+  }
   if (g.vec == 4)
     MRP_LAUNCH((mrp::film_fwd_regular<NT, KMAX, 4>), lds);
   else if (g.vec == 1)

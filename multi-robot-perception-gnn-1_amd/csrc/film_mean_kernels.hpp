@@ -592,8 +592,14 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
 // workgroups (the prologue is two rounds of loads: edge ids, then gamma/beta, both in flight
 // together with the first slice).
 // ---------------------------------------------------------------------------
-template <int NT, int KMAX, int VEC>
+//
+// KC > 0: the in-degree is the compile-time KC (a power of two; the launcher checks a.kdeg == KC) and
+// the mode is a mean: the slot loop has no exit test and the mean's division is the exact product
+// by 1/KC (x * 2^-k is the correctly rounded x / 2^k), instead of the ~10-instruction IEEE division
+// per destination and element.  KC = 0: runtime K and mode.
+template <int NT, int KMAX, int VEC, int KC = 0>
 __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
+  static_assert(KC == 0 || (KC <= KMAX && (KC & (KC - 1)) == 0), "compile-time degree: a power of two");
   constexpr int NS = NT * KMAX;
   constexpr int WS = NS + 2;     // per-channel stride of the slot weights (float2), padded 4 banks
   constexpr int WPD = KMAX / 4;  // 32-bit words of packed 8-bit slot sources per destination
@@ -614,7 +620,7 @@ __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
   const int n = min(a.goff[b + 1] - node0, NT);
   if (n <= 0) return;
   const int c0 = cb * a.cpb;
-  const int K = a.kdeg;
+  const int K = KC > 0 ? KC : a.kdeg;
 
   const int grp = threadIdx.x / a.lpc;
   const int li = threadIdx.x - grp * a.lpc;
@@ -731,14 +737,18 @@ __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
 #pragma unroll
-      for (int jj = 0; jj < KMAX; ++jj) {
-        if (jj >= K) break;  // wave-uniform
+      for (int jj = 0; jj < (KC > 0 ? KC : KMAX); ++jj) {
+        if (KC == 0 && jj >= K) break;  // wave-uniform
         const int u = (uw[jj >> 2] >> (8 * (jj & 3))) & 0xffu;
         const float2 w = Wc[v * KMAX + jj];
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc[k] = __fadd_rn(acc[k], __fadd_rn(__fmul_rn(w.x, xs[k][u]), w.y));
       }
-      if (mean) {
+      if constexpr (KC > 0) {
+        constexpr float r = 1.0f / (float)KC;  // exact: KC is a power of two
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[k] = __fmul_rn(acc[k], r);
+      } else if (mean) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc[k] = acc[k] / d;
       }

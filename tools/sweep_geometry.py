@@ -57,13 +57,14 @@ def fwd_time(g, z, csr):
     return t, alg_bytes_fwd(Nt, g.num_edges(), C, H * W) / t / 8e12
 
 
-def bwd_time(g, z, csr):
+def bwd_time(g, z, csr, need_dx=True, need_dgb=True):
     x = g.ndata["image"]
     Nt, C, H, W = x.shape
     plane = x.numel() * 4
     nb = rotating_sets(3 * plane)
     sets = [(torch.randn_like(x), x if i == 0 else torch.randn_like(x)) for i in range(nb)]
-    launches = [lambda G=G, a=a: mrp.aggregate.film_mean_backward(G, a, z, csr, MODE, True, True) for G, a in sets]
+    launches = [lambda G=G, a=a: mrp.aggregate.film_mean_backward(G, a, z, csr, MODE, need_dx, need_dgb)
+                for G, a in sets]
     t = time_launches(launches, ITERS, dev)
     return t, alg_bytes_bwd(Nt, g.num_edges(), C, H * W) / t / 8e12
 
@@ -114,6 +115,16 @@ def main():
         for _ in range(3):
             sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0]})
             sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [2]})
+        return
+    if what == "cfg4fwdgeo":  # k-NN forward geometry after the compile-time-degree specialisation
+        sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0, 1], "fwd_regular_lo": [16, 32, 64],
+                                        "fwd_regular_hi": [32, 64], "fwd_regular_cap": [4, 8, 16]})
+        return
+    if what == "bwdparts":  # the backward's two halves alone: grad_x only, d gamma/beta only
+        for name in ("cfg4", "cfg1", "cfg3"):
+            for dx, dgb in ((True, True), (True, False), (False, True)):
+                sweep(f"bwd dx={int(dx)} dgb={int(dgb)}", name,
+                      lambda g, z, csr, dx=dx, dgb=dgb: bwd_time(g, z, csr, dx, dgb), {"bwd_regular_vec": [2]})
         return
     if what == "pre2":  # backward with / without the two-slice prefetch
         for name in ("north_star", "cfg1", "cfg2", "cfg3"):
