@@ -52,6 +52,16 @@ hipError_t launch_bwd_ntb(const AggArgs& a_in, const Geometry& g, hipStream_t st
 
 template <int NT, int KMAX, bool DXB>
 hipError_t launch_bwd_regular(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  if (g.vec == 4) {  // the matrix-core form (mrp_film_mean_bwd_ex chose it: P % 64 == 0, aligned)
+    const int cpw = g.cpb / 4;
+    if (cpw == 1)
+      MRP_LAUNCH((mrp::film_bwd_regular_mfma<KMAX, DXB, 1>), lds_regular_mfma<KMAX>(1));
+    else if (cpw == 2)
+      MRP_LAUNCH((mrp::film_bwd_regular_mfma<KMAX, DXB, 2>), lds_regular_mfma<KMAX>(2));
+    else
+      MRP_LAUNCH((mrp::film_bwd_regular_mfma<KMAX, DXB, 4>), lds_regular_mfma<KMAX>(4));
+    return hipGetLastError();
+  }
   // VEC 4 would need 4*NT registers more per operand and spills; KMAX 8 only fits at VEC 1
   const size_t lds = lds_regular<NT, KMAX>(g.cpb);
   bool done = false;

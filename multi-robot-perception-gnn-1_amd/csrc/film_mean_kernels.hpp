@@ -1453,6 +1453,244 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular_reduce(AggArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Backward for REGULAR graphs of up to 16 nodes on the matrix cores (film_bwd_regular's math):
+//   grad_x[u][p] = sum_v Wt[u][v] G[v][p]              (Wt[u][v] = s_v * sum of gamma over u->v)
+//   D[v][u]      = sum_p G[v][p] x[u][p]               (the per-channel Gram; slot (v, j) reads D[v][u(v,j)])
+//   S[v]         = sum_p G[v][p]
+// both products as v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation), graphs padded to
+// 16 nodes.  One wave = one channel plane of one graph (workgroup: 4 channels), pixels in groups of 64.
+// Why: film_bwd_regular keeps N*K Gram accumulators per lane next to both operand slices (~180 VGPRs,
+// 2 waves/SIMD) and walks each plane serially; here the Gram is 4 accumulator registers per lane, so
+// the wave holds two pixel groups of loads in flight at ~100 VGPRs.
+//
+// Register layouts (lane l, q = l >> 4, j = l & 15; MFMA: A[i][k] at lane (i = j, k = q), B[k][col] at
+// lane (k = q, col = j), C[4q + r][j] at lane l, element r):
+//   G, "by quad":  gq[b] = G[node 4q + b][64 g + 4 j .. +3]   (b = 0..3: four 256-byte rows per load)
+//     -> grad_x MFMA #c (c = pixel within the float4): A = Wt[j][4 q + b], B = gq[b][c], summed over b:
+//        C[u = 4q + r][col j] = grad_x[4q + r][64 g + 4 j + c]: four float4 stores of 256-byte rows, and
+//        the residual term self_scale * G[u] of element r is gq[r][c] in the same lane.
+//   x, "by node":  xn[t] = x[node j][64 g + 16 t + 4 q .. +3]  (t = 0..3)
+//   G by node: gq transposed through a per-wave LDS tile (in-wave ordering, no barrier)
+//     -> Gram MFMA (t, c): A = G by node [t][c] (i = v = j, k = q), B = xn[t][c] (k = q, col = u = j).
+// Nodes past the graph's n: G rows are zeroed (they would reach grad_x through zero weights as 0 * inf),
+// x rows are clamped loads that only touch unused Gram columns.
+// Requirements (launcher): P % 64 == 0, 16-byte aligned operands and node strides % 4 == 0.
+// ---------------------------------------------------------------------------
+typedef float mf4 __attribute__((ext_vector_type(4)));
+
+// CPW: channel planes per wave, walked in turn with the loads of the next (channel, pixel group)
+// issued before the current group's MFMAs (workgroup = 4 waves = 4 CPW channels; one prologue per
+// workgroup).  At CPW = 2 the configs[4] grid is 4096 waves: one round at 4 waves/SIMD.
+template <int KMAX, bool DXB, int CPW>
+__global__ void __launch_bounds__(kBlock) film_bwd_regular_mfma(AggArgs a) {
+  constexpr int NT = 16, CPB = 4 * CPW;  // nodes (padded), channels per workgroup
+  constexpr int NS = NT * KMAX;
+  constexpr int WR = NT + 1;             // Wt / D row stride (floats)
+  constexpr int TR = 32 + 4;             // transpose tile row stride: 32 pixels + 4 (rows 4 banks apart)
+  extern __shared__ float4 smem_f4[];
+  float* smem = reinterpret_cast<float*>(smem_f4);
+  float* Wt = smem;                   // [CPB][NT][WR]  Wt[u][v]; each channel's rows become D[v][u]
+  float* Tt = Wt + CPB * NT * WR;     // [4][NT][TR]    per-wave transpose tile (half a pixel group)
+  float* Sl = Tt + 4 * NT * TR;       // [CPB][NT]
+  int* slot_u = reinterpret_cast<int*>(Sl + CPB * NT);  // [NS]
+  int* slot_e = slot_u + NS;                             // [NS]
+
+  const int b = blockIdx.x / a.ncb;
+  const int cb = blockIdx.x - b * a.ncb;
+  const int node0 = a.goff[b];
+  const int n = min(a.goff[b + 1] - node0, NT);
+  if (n <= 0) return;
+  const int c0 = cb * CPB;
+  const int K = a.kdeg;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = lane >> 4, jl = lane & 15;
+  float s = a.mode != MRP_AGG_FILM_SUM && K > 0 ? 1.f / (float)K : 1.f;
+  s *= a.agg_scale;  // epilogue: grad_out reaches the aggregate scaled
+
+  // ---- prologue: thread t owns (channel t % CPB, destination t / CPB): column v of that channel's
+  // Wt and (channel 0) v's slot row.  Sources / edge ids first, gamma after (dependent loads).
+  for (int t = threadIdx.x; t < CPB * NT; t += blockDim.x) {
+    const int cl = t % CPB, v = t / CPB;
+    const bool ok = v < n && c0 + cl < a.C;
+    int us[KMAX], es[KMAX];
+#pragma unroll
+    for (int jj = 0; jj < KMAX; ++jj) {
+      const bool on = ok && jj < K;
+      const int k = (node0 + (on ? v : 0)) * K + (on ? jj : 0);
+      us[jj] = on ? a.src[k] - node0 : -1;
+      es[jj] = on ? a.eid[k] : -1;
+    }
+    float gm[KMAX];
+#pragma unroll
+    for (int jj = 0; jj < KMAX; ++jj) {
+      gm[jj] = 0.f;
+      if (es[jj] >= 0) {
+        if (a.mode == MRP_AGG_COPY_MEAN) {
+          gm[jj] = 1.f;
+        } else {
+          gm[jj] = a.gb[((int64_t)es[jj] * a.C + c0 + cl) * 2];
+          if (a.logits) gm[jj] = sigmoidf(gm[jj]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      float wv = 0.f;  // += in slot order: multi-edges sum like the CSR tile build
+#pragma unroll
+      for (int jj = 0; jj < KMAX; ++jj)
+        if (us[jj] == u) wv += s * gm[jj];
+      Wt[(cl * NT + u) * WR + v] = wv;
+    }
+    if (cl == 0) {
+#pragma unroll
+      for (int jj = 0; jj < KMAX; ++jj) {
+        const bool in = (unsigned)us[jj] < (unsigned)n;  // outside the graph: rejected on the host
+        slot_u[v * KMAX + jj] = in ? us[jj] : 0;
+        slot_e[v * KMAX + jj] = in ? es[jj] : -1;
+      }
+    }
+  }
+  __syncthreads();
+
+  // this lane's row offsets (bytes, 32-bit: the host checks 15 strides + a plane fit)
+  uint32_t goff4[4], boff4[4], ooff4[4];
+  bool gvalid[4];
+#pragma unroll
+  for (int bb = 0; bb < 4; ++bb) {
+    const int node = 4 * q + bb;
+    gvalid[bb] = node < n;
+    const uint32_t nd = (uint32_t)min(node, n - 1);
+    goff4[bb] = nd * (uint32_t)a.gs * 4u + (uint32_t)jl * 16u;
+    ooff4[bb] = nd * (uint32_t)a.os * 4u + (uint32_t)jl * 16u;
+    boff4[bb] = DXB ? nd * (uint32_t)a.dxbs * 4u + (uint32_t)jl * 16u : 0u;
+  }
+  const uint32_t xoff = (uint32_t)min(jl, n - 1) * (uint32_t)a.xs * 4u + (uint32_t)q * 16u;
+  const int ngroups = a.P >> 6;
+  float* T = Tt + w * NT * TR;
+  // the wave's channels: c0 + w + 4 i, i < nch
+  const int nch = max(0, min(CPW, (a.C - c0 - w + 3) / 4));
+  const int nsteps = nch * ngroups;
+  auto chan = [&](int i) { return c0 + w + 4 * i; };
+
+  mf4 gq[4], xn[4], gq2[4], xn2[4];
+  auto load_step = [&](int st, mf4 (&gr)[4], mf4 (&xr)[4]) {
+    const int i = st / ngroups, g = st - i * ngroups;
+    const int c = chan(i);
+    const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c * a.P;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+      gr[bb] = __builtin_nontemporal_load(reinterpret_cast<const mf4*>(at_bytes(gbase, goff4[bb] + (uint32_t)g * 256u)));
+    if (a.want_dgb) {
+      const float* xbase = a.x + (int64_t)node0 * a.xs + (int64_t)c * a.P;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        xr[t] = __builtin_nontemporal_load(
+            reinterpret_cast<const mf4*>(at_bytes(xbase, xoff + (uint32_t)g * 256u + (uint32_t)t * 64u)));
+    }
+  };
+
+  float wa[4];
+  mf4 dacc = {0.f, 0.f, 0.f, 0.f};  // Gram: D[4q + r][jl] of the current channel
+  float sacc = 0.f;                 // S partial: node jl, this lane's pixels
+  auto compute_step = [&](int st, mf4 (&gr)[4], const mf4 (&xr)[4]) {
+    const int i = st / ngroups, g = st - i * ngroups;
+    const int cl = w + 4 * i;  // channel within the workgroup
+    const int c = c0 + cl;
+    if (g == 0) {
+      // A operand of the grad_x MFMAs: Wt[u = jl][v = 4 q + bb]
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) wa[bb] = Wt[(cl * NT + jl) * WR + 4 * q + bb];
+      dacc = mf4{0.f, 0.f, 0.f, 0.f};
+      sacc = 0.f;
+    }
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+      if (!gvalid[bb]) gr[bb] = mf4{0.f, 0.f, 0.f, 0.f};
+    if (a.want_dx) {
+      float* obase = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
+      const float* dxbase = DXB ? a.dxb + (int64_t)node0 * a.dxbs + (int64_t)c * a.P : nullptr;
+      mf4 acc[4];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        acc[cc] = mf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) acc[cc] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[bb], gr[bb][cc], acc[cc], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        mf4 o = {acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
+        if (a.self_scale != 0.f) o += a.self_scale * gr[r];  // residual epilogue
+        if (gvalid[r]) {
+          if (DXB) o += __builtin_nontemporal_load(reinterpret_cast<const mf4*>(at_bytes(dxbase, boff4[r] + (uint32_t)g * 256u)));
+          __builtin_nontemporal_store(o, reinterpret_cast<mf4*>(at_bytes(obase, ooff4[r] + (uint32_t)g * 256u)));
+        }
+      }
+    }
+    if (a.want_dgb) {
+      // G by node through the wave's LDS tile, 32 pixels (two t) at a time
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if ((jl >> 3) == h) {  // lanes with jl in [8h, 8h + 8) hold pixels [32h, 32h + 32) of the group
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb) *reinterpret_cast<mf4*>(T + (4 * q + bb) * TR + 4 * (jl & 7)) = gr[bb];
+        }
+        // the tile is exchanged between lanes of this wave only: LDS executes a wave's accesses in
+        // order, so a compiler-level barrier (no reordering across it) is all the ordering needed
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2) {
+          const mf4 gn = *reinterpret_cast<const mf4*>(T + jl * TR + 16 * t2 + 4 * q);
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc)
+            dacc = __builtin_amdgcn_mfma_f32_16x16x4f32(gn[cc], xr[2 * h + t2][cc], dacc, 0, 0, 0);
+          sacc += (gn[0] + gn[1]) + (gn[2] + gn[3]);
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (g == ngroups - 1) {
+        // the channel is done: its Wt rows (read into wa at g == 0 by this wave only) become D[v][u]
+        sacc += __shfl_xor(sacc, 16, 64);
+        sacc += __shfl_xor(sacc, 32, 64);
+        float* Dw = Wt + cl * NT * WR;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Dw[(4 * q + r) * WR + jl] = dacc[r];
+        if (q == 0) Sl[cl * NT + jl] = sacc;
+      }
+    }
+  };
+
+  // software pipeline over the wave's (channel, pixel group) steps: two register sets, the next
+  // step's loads in flight under the current step's MFMAs
+  if (nsteps > 0) load_step(0, gq, xn);
+  for (int st = 0; st < nsteps; st += 2) {
+    if (st + 1 < nsteps) load_step(st + 1, gq2, xn2);
+    compute_step(st, gq, xn);
+    if (st + 1 < nsteps) {
+      if (st + 2 < nsteps) load_step(st + 2, gq, xn);
+      compute_step(st + 1, gq2, xn2);
+    }
+  }
+  if (!a.want_dgb) return;
+  __syncthreads();
+  // per-edge outputs: thread -> (channel fastest, slot)
+  for (int t = threadIdx.x; t < CPB * NS; t += blockDim.x) {
+    const int cl = t % CPB, slot = t / CPB;
+    const int v = slot / KMAX;
+    const int cc = c0 + cl;
+    const int e = slot_e[slot];
+    if (e < 0 || cc >= a.C) continue;
+    const int u = slot_u[slot];
+    const int64_t off = ((int64_t)e * a.C + cc) * 2;
+    float2 r = make_float2(s * Wt[(cl * NT + v) * WR + u], s * Sl[cl * NT + v]);
+    if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
+    *reinterpret_cast<float2*>(a.dgb + off) = r;
+  }
+}
+
 }  // namespace mrp
 
 // ===========================================================================
@@ -1481,6 +1719,10 @@ struct Tuning {
   int bwd_fused_lo = 8, bwd_fused_hi = 128, bwd_fused_cap = 8;
   int bwd_pre2 = 1;  // film_bwd_fused: prefetch both slices when a lane owns exactly two
   int bwd_regular_vec = 2, bwd_regular_lanes = 16;              // film_bwd_regular (N > 8, k-NN)
+  // film_bwd_regular_mfma (regular graphs of 9..16 nodes, P % 64 == 0, 16-byte aligned): Gram and
+  // grad_x on the matrix cores; 0 = film_bwd_regular everywhere
+  int bwd_regular_mfma = 1;
+  int bwd_mfma_cpw = 2;  // film_bwd_regular_mfma: channel planes per wave (1, 2 or 4)
   // film_bwd_regular: split planes so each lane owns this many slices (0: whole planes); needs the
   // caller's workspace (mrp_film_mean_bwd_workspace), else whole planes.  Measured slower at the
   // configs[4] shape (k-NN(4) N=16 C=1024 16x16 B=8: 102.7 us whole planes, 113 / 131 / 170 us at
@@ -1533,6 +1775,10 @@ size_t lds_regular(int cpb) {
   return (size_t)(cpb * mrp::Tile<NT>::SZ + cpb * NT * KMAX + cpb * mrp::Tile<NT>::NTP + mrp::Tile<NT>::NTP) *
              sizeof(float) +
          2 * (size_t)NT * KMAX * sizeof(int);
+}
+template <int KMAX>
+size_t lds_regular_mfma(int cpw) {
+  return (size_t)(4 * cpw * 16 * 17 + 4 * 16 * 36 + 4 * cpw * 16) * sizeof(float) + 2 * (size_t)16 * KMAX * sizeof(int);
 }
 template <int NT>
 size_t lds_bwd(int cpb, bool complete_logits, int lpc = 64) {

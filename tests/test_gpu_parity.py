@@ -452,6 +452,8 @@ def test_regular_backward_plane_split_path(cuda_device, slices):
     G = torch.randn_like(x)
     res = []
     try:
+        # against the whole-plane VALU kernel (the matrix-core kernel sums in another order)
+        assert lib.mrp_tuning_set(b"bwd_regular_mfma", 0) == 0
         for knob in (0, slices):
             assert lib.mrp_tuning_set(b"bwd_regular_slices", knob) == 0
             xd = x.to(cuda_device).requires_grad_(True)

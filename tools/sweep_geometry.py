@@ -116,6 +116,13 @@ def main():
             sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0]})
             sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [2]})
         return
+    if what == "cfg4bwd":  # k-NN backward: matrix-core kernel against the VALU kernel
+        for _ in range(2):
+            sweep("bwd", "cfg4", bwd_time, {"bwd_regular_mfma": [0, 1], "bwd_mfma_cpw": [1, 2, 4]})
+        for dx, dgb in ((True, False), (False, True)):
+            sweep(f"bwd dx={int(dx)} dgb={int(dgb)}", "cfg4",
+                  lambda g, z, csr, dx=dx, dgb=dgb: bwd_time(g, z, csr, dx, dgb), {"bwd_regular_mfma": [0, 1]})
+        return
     if what == "cfg4fwdgeo":  # k-NN forward geometry after the compile-time-degree specialisation
         sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0, 1], "fwd_regular_lo": [16, 32, 64],
                                         "fwd_regular_hi": [32, 64], "fwd_regular_cap": [4, 8, 16]})
