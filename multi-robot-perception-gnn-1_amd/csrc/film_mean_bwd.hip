@@ -123,20 +123,24 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const flo
     const int ps = regular_psplit(g, P);
     if (ps > 1 && regular_ws_bytes(g, num_graphs, max_nodes, kdeg <= 4 ? 4 : 8, ps) <= workspace_bytes) psplit = ps;
   }
-  if (max_nodes > 8 && kdeg >= 1 && kdeg <= 8 && psplit == 1 && tuning().bwd_regular_mfma && vec4 && P % 64 == 0) {
-    // film_bwd_regular_mfma: one wave per channel plane, 4 channels per workgroup; its per-lane row
-    // offsets are 32-bit (15 node strides + a plane)
+  // film_bwd_mfma: regular graphs of 9..16 nodes and complete graphs, whole pixel groups of 64
+  const bool complete = graph_kind == MRP_GRAPH_COMPLETE;
+  const bool mfma_kind = (max_nodes > 8 && kdeg >= 1 && kdeg <= 8 && tuning().bwd_regular_mfma) ||
+                         (complete && max_nodes >= 2 && tuning().bwd_complete_mfma);
+  if (mfma_kind && psplit == 1 && vec4 && P % 64 == 0) {
+    // per-lane row offsets are 32-bit: 15 node strides + two planes (a block's channel pair)
     const int64_t lim = (int64_t)1 << 32;
-    const int64_t span = (int64_t)plane * 4;
+    const int64_t span = (int64_t)plane * 4 + (int64_t)P * 4;
     bool fits = (int64_t)15 * g_node_stride * 4 + span < lim;
     if (want_dx) fits = fits && (int64_t)15 * gx_node_stride * 4 + span < lim;
     if (want_dx && grad_x_base) fits = fits && (int64_t)15 * base_node_stride * 4 + span < lim;
     if (want_dgb) fits = fits && (int64_t)15 * x_node_stride * 4 + span < lim;
     if (fits) {
+      const int cpw = tuning().bwd_mfma_cpw >= 2 ? 2 : 1;  // instantiated: 1, 2
+      g.mfma_npb = max_nodes <= 8 && complete ? 8 : 16;
       g.vec = 4;
       g.lpc = 64;
-      const int cpw = tuning().bwd_mfma_cpw == 3 ? 2 : tuning().bwd_mfma_cpw;  // instantiated: 1, 2, 4
-      g.cpb = 4 * cpw;  // 4 waves x channels per wave
+      g.cpb = 4 * cpw * (16 / g.mfma_npb);  // 4 waves x blocks per wave x channels per block
       g.threads = 256;
       g.ncb = (C + g.cpb - 1) / g.cpb;
     }
@@ -174,6 +178,7 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const flo
   a.epi = (agg_scale != 1.f || self_scale != 0.f) ? 1 : 0;
   a.psplit = psplit;
   a.ws = psplit > 1 ? static_cast<float*>(workspace) : nullptr;
+  a.nmax = max_nodes;
   return dispatch_bwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, st);
 }
 

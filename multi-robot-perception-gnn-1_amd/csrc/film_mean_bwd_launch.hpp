@@ -52,16 +52,6 @@ hipError_t launch_bwd_ntb(const AggArgs& a_in, const Geometry& g, hipStream_t st
 
 template <int NT, int KMAX, bool DXB>
 hipError_t launch_bwd_regular(const AggArgs& a, const Geometry& g, hipStream_t st) {
-  if (g.vec == 4) {  // the matrix-core form (mrp_film_mean_bwd_ex chose it: P % 64 == 0, aligned)
-    const int cpw = g.cpb / 4;
-    if (cpw == 1)
-      MRP_LAUNCH((mrp::film_bwd_regular_mfma<KMAX, DXB, 1>), lds_regular_mfma<KMAX>(1));
-    else if (cpw == 2)
-      MRP_LAUNCH((mrp::film_bwd_regular_mfma<KMAX, DXB, 2>), lds_regular_mfma<KMAX>(2));
-    else
-      MRP_LAUNCH((mrp::film_bwd_regular_mfma<KMAX, DXB, 4>), lds_regular_mfma<KMAX>(4));
-    return hipGetLastError();
-  }
   // VEC 4 would need 4*NT registers more per operand and spills; KMAX 8 only fits at VEC 1
   const size_t lds = lds_regular<NT, KMAX>(g.cpb);
   bool done = false;
@@ -80,8 +70,46 @@ hipError_t launch_bwd_regular(const AggArgs& a, const Geometry& g, hipStream_t s
   return hipGetLastError();
 }
 
+// film_bwd_mfma (mrp_film_mean_bwd_ex chose it and set g.mfma_npb, g.cpb = 4 x blocks per wave x
+// channels per block)
+template <bool COMPLETE, int NPB, int KMAX>
+hipError_t launch_bwd_mfma_k(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  const size_t lds = lds_mfma(g.cpb, NPB, KMAX);
+  const int cpw = g.cpb / (4 * (16 / NPB));
+  if (a.dxb) {
+    if (cpw == 1)
+      MRP_LAUNCH((mrp::film_bwd_mfma<COMPLETE, NPB, KMAX, true, 1>), lds);
+    else
+      MRP_LAUNCH((mrp::film_bwd_mfma<COMPLETE, NPB, KMAX, true, 2>), lds);
+  } else {
+    if (cpw == 1)
+      MRP_LAUNCH((mrp::film_bwd_mfma<COMPLETE, NPB, KMAX, false, 1>), lds);
+    else
+      MRP_LAUNCH((mrp::film_bwd_mfma<COMPLETE, NPB, KMAX, false, 2>), lds);
+  }
+  return hipGetLastError();
+}
+
+
+template <int NT, bool COMPLETE>
+hipError_t launch_bwd_mfma(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  if constexpr (COMPLETE) {
+    if constexpr (NT <= 8)
+      return launch_bwd_mfma_k<true, 8, 1>(a, g, st);
+    else
+      return launch_bwd_mfma_k<true, 16, 1>(a, g, st);
+  } else {
+    if constexpr (NT > 8) {
+      if (a.kdeg >= 1 && a.kdeg <= 4) return launch_bwd_mfma_k<false, 16, 4>(a, g, st);
+      if (a.kdeg >= 5 && a.kdeg <= 8) return launch_bwd_mfma_k<false, 16, 8>(a, g, st);
+    }
+    return hipErrorInvalidValue;
+  }
+}
+
 template <int NT, bool COMPLETE>
 hipError_t launch_bwd_nt(const AggArgs& a, const Geometry& g, hipStream_t st) {
+  if (g.mfma_npb) return launch_bwd_mfma<NT, COMPLETE>(a, g, st);
   if constexpr (NT > 8 && !COMPLETE) {
     // regular in-degree (k-NN): per-edge-slot Gram, one sweep
     if (a.kdeg >= 1 && a.kdeg <= 4)

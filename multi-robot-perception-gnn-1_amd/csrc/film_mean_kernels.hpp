@@ -81,6 +81,7 @@ struct AggArgs {
   int64_t x0s;
   // backward of REGULAR graphs with psplit > 1: per-segment partial Grams, [graph][cb][seg][cpb][NS + NT]
   float* ws;
+  int32_t nmax;  // max_nodes (COMPLETE graphs: every graph's node count)
 };
 
 // Forward epilogue of destination `node`, channel c, slice at `off` (see AggArgs::epi).
@@ -1479,30 +1480,38 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular_reduce(AggArgs a) {
 // ---------------------------------------------------------------------------
 typedef float mf4 __attribute__((ext_vector_type(4)));
 
-// CPW: channel planes per wave, walked in turn with the loads of the next (channel, pixel group)
-// issued before the current group's MFMAs (workgroup = 4 waves = 4 CPW channels; one prologue per
-// workgroup).  At CPW = 2 the configs[4] grid is 4096 waves: one round at 4 waves/SIMD.
-template <int KMAX, bool DXB, int CPW>
-__global__ void __launch_bounds__(kBlock) film_bwd_regular_mfma(AggArgs a) {
-  constexpr int NT = 16, CPB = 4 * CPW;  // nodes (padded), channels per workgroup
-  constexpr int NS = NT * KMAX;
-  constexpr int WR = NT + 1;             // Wt / D row stride (floats)
-  constexpr int TR = 32 + 4;             // transpose tile row stride: 32 pixels + 4 (rows 4 banks apart)
+// Template parameters:
+//   COMPLETE: complete graphs of exactly n = max_nodes nodes with arithmetic edge ids (the reference
+//             topology), else REGULAR(k) graphs (slot (v, j) = CSR position K v + j).
+//   NPB:      nodes per 16-row block: 16 (graphs of 9..16 nodes, one channel per block) or 8 (graphs
+//             of <= 8 nodes: two channels share a block as a block-diagonal system; row/column
+//             16-index vn = 8 h + node, h = channel of the pair).
+//   CPW:      blocks per wave, walked in turn with the next (block, pixel group)'s loads in flight
+//             under the current group's MFMAs; workgroup = 4 waves = 4 CPW blocks, one prologue.
+template <bool COMPLETE, int NPB, int KMAX, bool DXB, int CPW>
+__global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
+  static_assert(NPB == 16 || NPB == 8, "16-row blocks of one or two channels");
+  constexpr int CB = 16 / NPB;             // channels per block
+  constexpr int CPB = 4 * CPW * CB;        // channels per workgroup
+  constexpr int NS = NPB * KMAX;           // REGULAR edge slots
+  constexpr int WR = NPB + 1;              // per-channel Wt / D row stride (floats)
+  constexpr int TR = 32 + 4;               // transpose tile row stride: 32 pixels + 4 (rows 4 banks apart)
   extern __shared__ float4 smem_f4[];
   float* smem = reinterpret_cast<float*>(smem_f4);
-  float* Wt = smem;                   // [CPB][NT][WR]  Wt[u][v]; each channel's rows become D[v][u]
-  float* Tt = Wt + CPB * NT * WR;     // [4][NT][TR]    per-wave transpose tile (half a pixel group)
-  float* Sl = Tt + 4 * NT * TR;       // [CPB][NT]
-  int* slot_u = reinterpret_cast<int*>(Sl + CPB * NT);  // [NS]
-  int* slot_e = slot_u + NS;                             // [NS]
+  float* Wt = smem;                   // [CPB][NPB][WR]  Wt[u][v]; each channel's rows become D[v][u]
+  float* Tt = Wt + CPB * NPB * WR;    // [4][16][TR]     per-wave transpose tile (half a pixel group)
+  float* Sl = Tt + 4 * 16 * TR;       // [CPB][NPB]
+  int* slot_u = reinterpret_cast<int*>(Sl + CPB * NPB);  // [NS] (REGULAR)
+  int* slot_e = slot_u + NS;                              // [NS]
 
   const int b = blockIdx.x / a.ncb;
   const int cb = blockIdx.x - b * a.ncb;
-  const int node0 = a.goff[b];
-  const int n = min(a.goff[b + 1] - node0, NT);
+  const int node0 = COMPLETE ? b * a.nmax : a.goff[b];
+  const int n = COMPLETE ? a.nmax : min(a.goff[b + 1] - node0, NPB);
   if (n <= 0) return;
   const int c0 = cb * CPB;
-  const int K = a.kdeg;
+  const int K = COMPLETE ? n - 1 : a.kdeg;
+  const int64_t ebase = (int64_t)b * n * (n - 1);  // COMPLETE: the graph's first edge
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int q = lane >> 4, jl = lane & 15;
@@ -1510,104 +1519,133 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular_mfma(AggArgs a) {
   s *= a.agg_scale;  // epilogue: grad_out reaches the aggregate scaled
 
   // ---- prologue: thread t owns (channel t % CPB, destination t / CPB): column v of that channel's
-  // Wt and (channel 0) v's slot row.  Sources / edge ids first, gamma after (dependent loads).
-  for (int t = threadIdx.x; t < CPB * NT; t += blockDim.x) {
+  // Wt (and, REGULAR, channel 0: v's slot row).  Index loads first, gamma after.
+  for (int t = threadIdx.x; t < CPB * NPB; t += blockDim.x) {
     const int cl = t % CPB, v = t / CPB;
     const bool ok = v < n && c0 + cl < a.C;
-    int us[KMAX], es[KMAX];
+    constexpr int NE = COMPLETE ? NPB : KMAX;  // candidate in-edges of v
+    int us[NE];
+    int64_t es[NE];
 #pragma unroll
-    for (int jj = 0; jj < KMAX; ++jj) {
-      const bool on = ok && jj < K;
-      const int k = (node0 + (on ? v : 0)) * K + (on ? jj : 0);
-      us[jj] = on ? a.src[k] - node0 : -1;
-      es[jj] = on ? a.eid[k] : -1;
+    for (int jj = 0; jj < NE; ++jj) {
+      if (COMPLETE) {
+        const bool on = ok && jj < n && jj != v;
+        us[jj] = on ? jj : -1;
+        es[jj] = on ? complete_eid(ebase, n, jj, v) : -1;
+      } else {
+        const bool on = ok && jj < K;
+        const int k = (node0 + (on ? v : 0)) * K + (on ? jj : 0);
+        us[jj] = on ? a.src[k] - node0 : -1;
+        es[jj] = on ? a.eid[k] : -1;
+      }
     }
-    float gm[KMAX];
+    float gm[NE];
 #pragma unroll
-    for (int jj = 0; jj < KMAX; ++jj) {
+    for (int jj = 0; jj < NE; ++jj) {
       gm[jj] = 0.f;
       if (es[jj] >= 0) {
         if (a.mode == MRP_AGG_COPY_MEAN) {
           gm[jj] = 1.f;
         } else {
-          gm[jj] = a.gb[((int64_t)es[jj] * a.C + c0 + cl) * 2];
+          gm[jj] = a.gb[(es[jj] * a.C + c0 + cl) * 2];
           if (a.logits) gm[jj] = sigmoidf(gm[jj]);
         }
       }
     }
 #pragma unroll
-    for (int u = 0; u < NT; ++u) {
-      float wv = 0.f;  // += in slot order: multi-edges sum like the CSR tile build
+    for (int u = 0; u < NPB; ++u) {
+      float wv = 0.f;
+      if (COMPLETE) {
+        wv = s * gm[u];
+      } else {
 #pragma unroll
-      for (int jj = 0; jj < KMAX; ++jj)
-        if (us[jj] == u) wv += s * gm[jj];
-      Wt[(cl * NT + u) * WR + v] = wv;
+        for (int jj = 0; jj < NE; ++jj)  // += in slot order: multi-edges sum like the CSR tile build
+          if (us[jj] == u) wv += s * gm[jj];
+      }
+      Wt[(cl * NPB + u) * WR + v] = wv;
     }
-    if (cl == 0) {
+    if (!COMPLETE && cl == 0) {
 #pragma unroll
       for (int jj = 0; jj < KMAX; ++jj) {
         const bool in = (unsigned)us[jj] < (unsigned)n;  // outside the graph: rejected on the host
         slot_u[v * KMAX + jj] = in ? us[jj] : 0;
-        slot_e[v * KMAX + jj] = in ? es[jj] : -1;
+        slot_e[v * KMAX + jj] = in ? (int)es[jj] : -1;
       }
     }
   }
   __syncthreads();
 
-  // this lane's row offsets (bytes, 32-bit: the host checks 15 strides + a plane fit)
+  // 16-row index vn -> (channel of the pair, node).  This lane's G rows: vn = 4q + bb; its x row: jl.
   uint32_t goff4[4], boff4[4], ooff4[4];
-  bool gvalid[4];
+  bool nvalid[4];
+  int hq[4];
 #pragma unroll
   for (int bb = 0; bb < 4; ++bb) {
-    const int node = 4 * q + bb;
-    gvalid[bb] = node < n;
+    const int vn = 4 * q + bb;
+    const int h = vn / NPB, node = vn % NPB;
+    hq[bb] = h;
+    nvalid[bb] = node < n;
     const uint32_t nd = (uint32_t)min(node, n - 1);
-    goff4[bb] = nd * (uint32_t)a.gs * 4u + (uint32_t)jl * 16u;
-    ooff4[bb] = nd * (uint32_t)a.os * 4u + (uint32_t)jl * 16u;
-    boff4[bb] = DXB ? nd * (uint32_t)a.dxbs * 4u + (uint32_t)jl * 16u : 0u;
+    const uint32_t hp = (uint32_t)h * (uint32_t)a.P * 4u + (uint32_t)jl * 16u;
+    goff4[bb] = nd * (uint32_t)a.gs * 4u + hp;
+    ooff4[bb] = nd * (uint32_t)a.os * 4u + hp;
+    boff4[bb] = DXB ? nd * (uint32_t)a.dxbs * 4u + hp : 0u;
   }
-  const uint32_t xoff = (uint32_t)min(jl, n - 1) * (uint32_t)a.xs * 4u + (uint32_t)q * 16u;
+  const int hx = jl / NPB, nx = jl % NPB;
   const int ngroups = a.P >> 6;
-  float* T = Tt + w * NT * TR;
-  // the wave's channels: c0 + w + 4 i, i < nch
-  const int nch = max(0, min(CPW, (a.C - c0 - w + 3) / 4));
-  const int nsteps = nch * ngroups;
-  auto chan = [&](int i) { return c0 + w + 4 * i; };
+  float* T = Tt + w * 16 * TR;
+  // the wave's blocks: channels c0 + (w + 4 i) CB + h
+  const int nblk = max(0, min(CPW, (a.C - c0 - w * CB + 4 * CB - 1) / (4 * CB)));
+  const int nsteps = nblk * ngroups;
+  auto blk_c = [&](int i) { return c0 + (w + 4 * i) * CB; };  // first channel of block i
+  // a block's second channel may lie past C (odd C): its loads then read the first channel's rows
+  auto hvalid = [&](int i, int h) { return blk_c(i) + h < a.C; };
 
   mf4 gq[4], xn[4], gq2[4], xn2[4];
   auto load_step = [&](int st, mf4 (&gr)[4], mf4 (&xr)[4]) {
     const int i = st / ngroups, g = st - i * ngroups;
-    const int c = chan(i);
+    const int c = blk_c(i);
     const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c * a.P;
+    const bool h1 = CB == 1 || hvalid(i, 1);
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb)
-      gr[bb] = __builtin_nontemporal_load(reinterpret_cast<const mf4*>(at_bytes(gbase, goff4[bb] + (uint32_t)g * 256u)));
+    for (int bb = 0; bb < 4; ++bb) {
+      const uint32_t off = goff4[bb] - (h1 ? 0u : (uint32_t)hq[bb] * (uint32_t)a.P * 4u);
+      gr[bb] = __builtin_nontemporal_load(reinterpret_cast<const mf4*>(at_bytes(gbase, off + (uint32_t)g * 256u)));
+    }
     if (a.want_dgb) {
       const float* xbase = a.x + (int64_t)node0 * a.xs + (int64_t)c * a.P;
+      const uint32_t xo = (uint32_t)min(nx, n - 1) * (uint32_t)a.xs * 4u + (uint32_t)(h1 ? hx : 0) * (uint32_t)a.P * 4u +
+                          (uint32_t)q * 16u;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         xr[t] = __builtin_nontemporal_load(
-            reinterpret_cast<const mf4*>(at_bytes(xbase, xoff + (uint32_t)g * 256u + (uint32_t)t * 64u)));
+            reinterpret_cast<const mf4*>(at_bytes(xbase, xo + (uint32_t)g * 256u + (uint32_t)t * 64u)));
     }
   };
 
   float wa[4];
-  mf4 dacc = {0.f, 0.f, 0.f, 0.f};  // Gram: D[4q + r][jl] of the current channel
-  float sacc = 0.f;                 // S partial: node jl, this lane's pixels
+  mf4 dacc = {0.f, 0.f, 0.f, 0.f};  // Gram: D[4q + r][jl] of the current block
+  float sacc = 0.f;                 // S partial: row jl, this lane's pixels
   auto compute_step = [&](int st, mf4 (&gr)[4], const mf4 (&xr)[4]) {
     const int i = st / ngroups, g = st - i * ngroups;
-    const int cl = w + 4 * i;  // channel within the workgroup
-    const int c = c0 + cl;
-    if (g == 0) {
-      // A operand of the grad_x MFMAs: Wt[u = jl][v = 4 q + bb]
+    const int cbl = (w + 4 * i) * CB;  // first channel of the block within the workgroup
+    const int c = c0 + cbl;
+    bool rvalid[4];
 #pragma unroll
-      for (int bb = 0; bb < 4; ++bb) wa[bb] = Wt[(cl * NT + jl) * WR + 4 * q + bb];
+    for (int bb = 0; bb < 4; ++bb) rvalid[bb] = nvalid[bb] && (CB == 1 || hvalid(i, hq[bb]));
+    if (g == 0) {
+      // A operand of the grad_x MFMAs: W[u = jl][v = 4 q + bb], zero off the block diagonal
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const int vn = 4 * q + bb;
+        wa[bb] = (jl / NPB == vn / NPB) ? Wt[((cbl + jl / NPB) * NPB + jl % NPB) * WR + vn % NPB] : 0.f;
+      }
       dacc = mf4{0.f, 0.f, 0.f, 0.f};
       sacc = 0.f;
     }
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb)
-      if (!gvalid[bb]) gr[bb] = mf4{0.f, 0.f, 0.f, 0.f};
+      if (!rvalid[bb]) gr[bb] = mf4{0.f, 0.f, 0.f, 0.f};
     if (a.want_dx) {
       float* obase = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
       const float* dxbase = DXB ? a.dxb + (int64_t)node0 * a.dxbs + (int64_t)c * a.P : nullptr;
@@ -1622,17 +1660,17 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular_mfma(AggArgs a) {
       for (int r = 0; r < 4; ++r) {
         mf4 o = {acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
         if (a.self_scale != 0.f) o += a.self_scale * gr[r];  // residual epilogue
-        if (gvalid[r]) {
+        if (rvalid[r]) {
           if (DXB) o += __builtin_nontemporal_load(reinterpret_cast<const mf4*>(at_bytes(dxbase, boff4[r] + (uint32_t)g * 256u)));
           __builtin_nontemporal_store(o, reinterpret_cast<mf4*>(at_bytes(obase, ooff4[r] + (uint32_t)g * 256u)));
         }
       }
     }
     if (a.want_dgb) {
-      // G by node through the wave's LDS tile, 32 pixels (two t) at a time
+      // G by row through the wave's LDS tile, 32 pixels (two t) at a time
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if ((jl >> 3) == h) {  // lanes with jl in [8h, 8h + 8) hold pixels [32h, 32h + 32) of the group
+      for (int hh = 0; hh < 2; ++hh) {
+        if ((jl >> 3) == hh) {  // lanes with jl in [8hh, 8hh + 8) hold pixels [32hh, 32hh + 32) of the group
 #pragma unroll
           for (int bb = 0; bb < 4; ++bb) *reinterpret_cast<mf4*>(T + (4 * q + bb) * TR + 4 * (jl & 7)) = gr[bb];
         }
@@ -1643,28 +1681,31 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular_mfma(AggArgs a) {
 #pragma unroll
         for (int t2 = 0; t2 < 2; ++t2) {
           const mf4 gn = *reinterpret_cast<const mf4*>(T + jl * TR + 16 * t2 + 4 * q);
+          const mf4 xv = xr[2 * hh + t2];
 #pragma unroll
-          for (int cc = 0; cc < 4; ++cc)
-            dacc = __builtin_amdgcn_mfma_f32_16x16x4f32(gn[cc], xr[2 * h + t2][cc], dacc, 0, 0, 0);
+          for (int cc = 0; cc < 4; ++cc) dacc = __builtin_amdgcn_mfma_f32_16x16x4f32(gn[cc], xv[cc], dacc, 0, 0, 0);
           sacc += (gn[0] + gn[1]) + (gn[2] + gn[3]);
         }
         asm volatile("" ::: "memory");
         __builtin_amdgcn_wave_barrier();
       }
       if (g == ngroups - 1) {
-        // the channel is done: its Wt rows (read into wa at g == 0 by this wave only) become D[v][u]
+        // the block is done: its channels' Wt rows (read into wa at g == 0, by this wave only) become
+        // D[v][u] (the diagonal blocks of the 16 x 16 Gram)
         sacc += __shfl_xor(sacc, 16, 64);
         sacc += __shfl_xor(sacc, 32, 64);
-        float* Dw = Wt + cl * NT * WR;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Dw[(4 * q + r) * WR + jl] = dacc[r];
-        if (q == 0) Sl[cl * NT + jl] = sacc;
+        for (int r = 0; r < 4; ++r) {
+          const int vn = 4 * q + r;
+          if (vn / NPB == jl / NPB) Wt[((cbl + vn / NPB) * NPB + vn % NPB) * WR + jl % NPB] = dacc[r];
+        }
+        if (q == 0) Sl[(cbl + hx) * NPB + nx] = sacc;
       }
     }
   };
 
-  // software pipeline over the wave's (channel, pixel group) steps: two register sets, the next
-  // step's loads in flight under the current step's MFMAs
+  // software pipeline over the wave's (block, pixel group) steps: two register sets, the next step's
+  // loads in flight under the current step's MFMAs
   if (nsteps > 0) load_step(0, gq, xn);
   for (int st = 0; st < nsteps; st += 2) {
     if (st + 1 < nsteps) load_step(st + 1, gq2, xn2);
@@ -1676,16 +1717,27 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular_mfma(AggArgs a) {
   }
   if (!a.want_dgb) return;
   __syncthreads();
-  // per-edge outputs: thread -> (channel fastest, slot)
-  for (int t = threadIdx.x; t < CPB * NS; t += blockDim.x) {
-    const int cl = t % CPB, slot = t / CPB;
-    const int v = slot / KMAX;
+  // per-edge outputs: thread -> (channel fastest, edge)
+  const int nedge = COMPLETE ? n * (n - 1) : NS;
+  for (int t = threadIdx.x; t < CPB * nedge; t += blockDim.x) {
+    const int cl = t % CPB, el = t / CPB;
     const int cc = c0 + cl;
-    const int e = slot_e[slot];
-    if (e < 0 || cc >= a.C) continue;
-    const int u = slot_u[slot];
-    const int64_t off = ((int64_t)e * a.C + cc) * 2;
-    float2 r = make_float2(s * Wt[(cl * NT + v) * WR + u], s * Sl[cl * NT + v]);
+    if (cc >= a.C) continue;
+    int u, v;
+    int64_t e;
+    if (COMPLETE) {
+      u = el / (n - 1);
+      const int vi = el - u * (n - 1);
+      v = vi < u ? vi : vi + 1;
+      e = ebase + el;
+    } else {
+      v = el / KMAX;
+      e = slot_e[el];
+      u = slot_u[el];
+      if (e < 0) continue;
+    }
+    const int64_t off = (e * a.C + cc) * 2;
+    float2 r = make_float2(s * Wt[(cl * NPB + v) * WR + u], s * Sl[cl * NPB + v]);
     if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
     *reinterpret_cast<float2*>(a.dgb + off) = r;
   }
@@ -1703,6 +1755,7 @@ using mrp::AggArgs;
 struct Geometry {
   int vec, lpc, cpb, threads, ncb;
   int64_t grid;
+  int mfma_npb = 0;  // film_bwd_mfma: nodes per 16-row block (16 or 8); 0 = the VALU kernels
 };
 
 // Launch geometry knobs (defaults = the measured optima; mrp_tuning_set changes them for lab sweeps).
@@ -1719,10 +1772,12 @@ struct Tuning {
   int bwd_fused_lo = 8, bwd_fused_hi = 128, bwd_fused_cap = 8;
   int bwd_pre2 = 1;  // film_bwd_fused: prefetch both slices when a lane owns exactly two
   int bwd_regular_vec = 2, bwd_regular_lanes = 16;              // film_bwd_regular (N > 8, k-NN)
-  // film_bwd_regular_mfma (regular graphs of 9..16 nodes, P % 64 == 0, 16-byte aligned): Gram and
-  // grad_x on the matrix cores; 0 = film_bwd_regular everywhere
+  // film_bwd_mfma (Gram and grad_x on the matrix cores; P % 64 == 0, 16-byte aligned operands):
+  // regular graphs of 9..16 nodes (0 = film_bwd_regular), complete graphs (1; default 0: film_bwd_fused
+  // measured faster at every config: 143 vs 159 us at configs[1], 59 vs 64 at [2], 27 vs 29 at [3])
   int bwd_regular_mfma = 1;
-  int bwd_mfma_cpw = 2;  // film_bwd_regular_mfma: channel planes per wave (1, 2 or 4)
+  int bwd_complete_mfma = 0;
+  int bwd_mfma_cpw = 2;  // film_bwd_mfma: 16-row blocks per wave (1 or 2)
   // film_bwd_regular: split planes so each lane owns this many slices (0: whole planes); needs the
   // caller's workspace (mrp_film_mean_bwd_workspace), else whole planes.  Measured slower at the
   // configs[4] shape (k-NN(4) N=16 C=1024 16x16 B=8: 102.7 us whole planes, 113 / 131 / 170 us at
@@ -1776,9 +1831,9 @@ size_t lds_regular(int cpb) {
              sizeof(float) +
          2 * (size_t)NT * KMAX * sizeof(int);
 }
-template <int KMAX>
-size_t lds_regular_mfma(int cpw) {
-  return (size_t)(4 * cpw * 16 * 17 + 4 * 16 * 36 + 4 * cpw * 16) * sizeof(float) + 2 * (size_t)16 * KMAX * sizeof(int);
+// film_bwd_mfma: Wt/D + transpose tiles + S + slot table (cpb channels of npb nodes)
+inline size_t lds_mfma(int cpb, int npb, int kmax) {
+  return (size_t)(cpb * npb * (npb + 1) + 4 * 16 * 36 + cpb * npb) * sizeof(float) + 2 * (size_t)npb * kmax * sizeof(int);
 }
 template <int NT>
 size_t lds_bwd(int cpb, bool complete_logits, int lpc = 64) {

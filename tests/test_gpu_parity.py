@@ -468,3 +468,37 @@ def test_regular_backward_plane_split_path(cuda_device, slices):
     _, dgb_ref = oracle.film_aggregate_grads(x, torch.sigmoid(gb), src, dst, G)
     dz_ref = dgb_ref * torch.sigmoid(gb) * (1 - torch.sigmoid(gb))
     assert rel_err(res[1][1].numpy(), dz_ref.numpy()) <= TOL
+
+
+@pytest.mark.parametrize("n,C,hw,knn", [(8, 23, (8, 8), None), (5, 16, (16, 16), None), (12, 9, (8, 8), None),
+                                         (16, 13, (8, 8), 4), (11, 6, (16, 16), 6)])
+@pytest.mark.parametrize("combine", ["cat", "residual"])
+def test_mfma_backward_matches_valu_kernels(cuda_device, n, C, hw, knn, combine):
+    """film_bwd_mfma (Gram and grad_x on the matrix cores; the default for k-NN graphs of 9..16 nodes,
+    an opt-in for complete graphs) against the VALU kernels (film_bwd_fused / film_bwd_regular) and the
+    oracle: odd channel counts (a channel pair with one channel past C), graphs of 5..16 nodes, the
+    cat backward's grad_x base and the residual epilogue's self term."""
+    lib = m.load_library()
+    g, x, gb = random_case(n, C, hw[0], hw[1], seed=n * 7 + C, knn=knn, bnn=[n, n, n])
+    csr = g.csr(cuda_device)
+    op = m.film_mean_cat if combine == "cat" else m.film_mean_residual
+    G = torch.randn(op(x.to(cuda_device), gb.to(cuda_device), csr, logits=True).shape)
+    res = []
+    try:
+        for on in (0, 1):
+            assert lib.mrp_tuning_set(b"bwd_regular_mfma", on) == 0
+            assert lib.mrp_tuning_set(b"bwd_complete_mfma", on) == 0
+            xd = x.to(cuda_device).requires_grad_(True)
+            zd = gb.to(cuda_device).requires_grad_(True)
+            op(xd, zd, csr, logits=True).backward(G.to(cuda_device))
+            res.append((xd.grad.cpu(), zd.grad.cpu()))
+    finally:
+        lib.mrp_tuning_set(b"reset", 0)
+    assert rel_err(res[1][0].numpy(), res[0][0].numpy()) <= 1e-6
+    assert rel_err(res[1][1].numpy(), res[0][1].numpy()) <= 1e-6
+    src, dst = (t.numpy() for t in g.edges())
+    dx_ref, dgb_ref = oracle.film_aggregate_grads(x, torch.sigmoid(gb), src, dst, G[:, C:] if combine == "cat" else G)
+    dx_ref = dx_ref + (G[:, :C] if combine == "cat" else G)
+    dz_ref = dgb_ref * torch.sigmoid(gb) * (1 - torch.sigmoid(gb))
+    assert rel_err(res[1][0].numpy(), dx_ref.numpy()) <= TOL
+    assert rel_err(res[1][1].numpy(), dz_ref.numpy()) <= TOL

@@ -123,6 +123,12 @@ def main():
             sweep(f"bwd dx={int(dx)} dgb={int(dgb)}", "cfg4",
                   lambda g, z, csr, dx=dx, dgb=dgb: bwd_time(g, z, csr, dx, dgb), {"bwd_regular_mfma": [0, 1]})
         return
+    if what == "mfmabwd":  # complete graphs: matrix-core backward against film_bwd_fused
+        for name in ("cfg3", "cfg2", "cfg1"):
+            sweep("bwd", name, bwd_time, {"bwd_complete_mfma": [0]})
+            sweep("bwd", name, bwd_time, {"bwd_complete_mfma": [1], "bwd_mfma_cpw": [1, 2]})
+        sweep("bwd", "cfg4", bwd_time, {"bwd_regular_mfma": [1], "bwd_mfma_cpw": [1, 2]})
+        return
     if what == "cfg4fwdgeo":  # k-NN forward geometry after the compile-time-degree specialisation
         sweep("fwd", "cfg4", fwd_time, {"fwd_regular_split": [0, 1], "fwd_regular_lo": [16, 32, 64],
                                         "fwd_regular_hi": [32, 64], "fwd_regular_cap": [4, 8, 16]})
