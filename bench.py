@@ -374,7 +374,8 @@ def config_record(cid, world, rank, device, args):
 
     launches = [lambda G=G, xi=xi: bwd(G, xi) for G, xi in bsets]
     tb = time_launches(launches, args.kernel_iters, device)
-    bname = ("film_bwd_regular" if knn and N > 8 else "film_bwd_fused")
+    # k-NN graphs of > 8 nodes: the matrix-core backward (whole 64-pixel groups), else the VALU kernels
+    bname = (("film_bwd_mfma" if P % 64 == 0 else "film_bwd_regular") if knn and N > 8 else "film_bwd_fused")
     rec["roofline_bwd"] = roofline(bname, alg_bytes_bwd(Nt, E, C, P), tb, rotating_sets=nb,
                                    footprint_mb=round(nb * (3 * plane) / 2**20))
     del bsets, launches

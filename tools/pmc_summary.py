@@ -107,7 +107,7 @@ def main(src, rnd, iters=20, pmc_iters=5):
              "kernel": kname, "dispatches_traced": len(rec["durations_us"]),
              "avg_duration_us_trace": statistics.mean(rec["durations_us"]) if rec["durations_us"] else None,
              "vgpr_count_trace": rec.get("vgpr"), "grid": rec.get("grid")}
-        if kind == "fwd" or "bwd_fused" in kname or "bwd_regular" in kname:
+        if kind == "fwd" or "bwd_fused" in kname or "bwd_regular" in kname or "bwd_mfma" in kname:
             d["alg_bytes_per_launch"] = alg_bytes(shapes[sname], kind)
         if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
             d["hbm_bytes_per_launch"] = (2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024
