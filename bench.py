@@ -304,25 +304,30 @@ def config_record(cid, world, rank, device, args):
     rec = {"config": cfg["name"], "graphs_per_rank": hi - lo, "share": share, "robots": N, "channels": C,
            "H": H, "W": H, "layers": layers, "graph": f"k-NN({knn})" if knn else "complete",
            "graph_kind": "regular" if knn else "complete", "scaling": scaling}
-    with torch.no_grad():
-        fwd = lambda: net(g, x)  # noqa: E731
-        for _ in range(3):
-            fwd()
-        t = timed(fwd, args.config_steps, world, device, args.dist_backend)
-    rec["forward"] = {"value": world * elems / t if scaling == "weak" else None, "unit": "elems/s",
-                      "ms_per_step": t * 1e3}
-    # which compress path the eval forward took, and the other one for comparison (models.py policy)
+    # the eval forward (models.py's compress policy) and, for comparison, the other compress path:
+    # timed alternately, three rounds each, median per path — the first timed block of a sequence
+    # runs a few % slow (clocks), which a single A-then-B comparison would credit to the path
     fused = (mrp.models.fused_compress_enabled(P)
              and mrp.compress.dual_compress_supported(net.conv1, x))
     prev = mrp.models.fused_compress_setting()
-    mrp.models.set_fused_compress(not fused)
+    fwd = lambda: net(g, x)  # noqa: E731
+    ts, ts_other = [], []
     try:
         with torch.no_grad():
-            for _ in range(2):
+            for _ in range(3):
                 fwd()
-            t_other = timed(fwd, args.config_steps, world, device, args.dist_backend)
+            for _ in range(3):
+                for other in (False, True):
+                    mrp.models.set_fused_compress(prev if not other else (not fused))
+                    for _ in range(2):
+                        fwd()
+                    (ts_other if other else ts).append(timed(fwd, args.config_steps, world, device,
+                                                             args.dist_backend))
     finally:
         mrp.models.set_fused_compress(prev)
+    t, t_other = sorted(ts)[1], sorted(ts_other)[1]
+    rec["forward"] = {"value": world * elems / t if scaling == "weak" else None, "unit": "elems/s",
+                      "ms_per_step": t * 1e3}
     rec["forward"]["compress"] = ("aggregate kernel + two-source MFMA compress (no cat buffer)" if fused
                                   else "cat kernel + library GEMM")
     rec["forward"]["ms_per_step_other_compress"] = t_other * 1e3

@@ -308,9 +308,13 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
                           float* edge_pose, int32_t* indptr, int32_t* src, int32_t* eid,
                           int32_t* graph_off, void* stream);
 
-/* Experiment knobs of the launchers (kernel-lab sweeps; not needed for normal use).  Returns
- * hipErrorInvalidValue for an unknown name.  "fwd_regular_split": 1 (default) splits each channel
- * plane of a MRP_GRAPH_REGULAR forward over several workgroups, 0 keeps whole planes. */
+/* Experiment knobs of the launchers (kernel-lab sweeps; not needed for normal use; process-wide,
+ * not thread-safe).  Returns hipErrorInvalidValue for an unknown name or a value out of range;
+ * "reset" restores every default.  Geometry: "fwd_lo"/"fwd_hi"/"fwd_cap", "fwd_regular_*",
+ * "bwd_fused_*", "bwd_regular_*"; kernel choice: "bwd_regular_mfma" (1, default: the matrix-core
+ * backward for MRP_GRAPH_REGULAR graphs of 9..16 nodes), "bwd_complete_mfma" (0, default: complete
+ * graphs keep the VALU backward), "bwd_mfma_cpw" (channel blocks per wave of the matrix-core
+ * backward, 1 or 2), "bwd_pre2", "fwd_regular_split" (0, default: whole planes). */
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 11 = this header: the

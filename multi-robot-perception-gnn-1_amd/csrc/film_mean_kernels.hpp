@@ -1766,10 +1766,11 @@ struct Tuning {
   // 57.0 us split over 2 workgroups with 32 lanes; tools/sweep_geometry.py)
   int fwd_regular_split = 0;
   int fwd_regular_lo = 32, fwd_regular_hi = 32, fwd_regular_cap = 16;
-  // film_bwd_fused (N <= 8): at most 8 channels per workgroup — at 8x8 planes one-wave workgroups,
-  // 4x as many, so loads of later workgroups overlap the Gram reduction and epilogue of earlier
-  // ones (C=1280 B=32: 60.8 against 67.2 us with 32 channels; 32x32 planes are unaffected: 2)
-  int bwd_fused_lo = 8, bwd_fused_hi = 128, bwd_fused_cap = 8;
+  // film_bwd_fused (N <= 8): at most 16 channels per workgroup — at 8x8 planes (8 lanes per plane)
+  // two-wave workgroups: configs[3] 24.3 vs 25.6 us with 8 channels, configs[2] 54.7-54.9 vs 55.2
+  // (tools/sweep_geometry.py smallbwd; 32 channels: 67.2 vs 60.8 us at C=1280 in round 1); 32x32
+  // planes are unaffected (2 channels of 128 lanes)
+  int bwd_fused_lo = 8, bwd_fused_hi = 128, bwd_fused_cap = 16;
   int bwd_pre2 = 1;  // film_bwd_fused: prefetch both slices when a lane owns exactly two
   int bwd_regular_vec = 2, bwd_regular_lanes = 16;              // film_bwd_regular (N > 8, k-NN)
   // film_bwd_mfma (Gram and grad_x on the matrix cores; P % 64 == 0, 16-byte aligned operands):

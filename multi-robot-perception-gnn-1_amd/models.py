@@ -180,12 +180,12 @@ class GCN(nn.Module):
 
 
 _FUSED_COMPRESS = ["auto"]
-# "auto": the concatenation-free compress (aggregate kernel + two-source MFMA GEMM) wherever it
-# covers the shape.  Measured per layer stack in bench.py (the same run, both paths): configs[1]
-# 2.44 vs 2.61 ms, configs[2] 1.00 vs 1.07, configs[3] 1.22 vs 1.27, configs[4] 3.34 vs 3.40 — the
-# GEMM alone ties the library's at 8x8 / 16x16 (tools/exp_compress_dual.py), and skipping the
-# concatenation's extra write and read decides it.  FUSED_MIN_PLANE stays as a knob (pixels).
-FUSED_MIN_PLANE = 0
+# "auto": the concatenation-free compress where it measured faster than cat kernel + library GEMM
+# (DESIGN.md §3.6): planes of >= 1024 pixels (configs[1], 32x32: aggregate 92 us + two-source GEMM
+# 1.05 ms = 1.14 ms vs 1.24 ms per layer); at 16x16 (configs[4]: 1.09 vs 1.07 ms) and 8x8
+# (configs[2] 0.85 vs 0.81 ms, [3] 0.54 vs 0.51 ms) the cat kernel + library GEMM stays
+# (tools/exp_compress_dual.py, both paths timed alternately on the same box)
+FUSED_MIN_PLANE = 1024
 
 
 def fused_compress_enabled(plane: int = None) -> bool:

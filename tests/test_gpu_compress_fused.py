@@ -6,8 +6,8 @@
   W = [I | 0] returns x itself.
 * Random weights: within max(1e-5, 4 x the fp32 restatement's error) of the float64 result
   (``tests/stack_ref.py``), as every other GEMM-bearing path.
-* The GCN stack in eval mode (no autograd) takes the concatenation-free path (forced on here; by default
-  wherever it covers the shape, models.FUSED_MIN_PLANE); its output matches the unfused (cat kernel + batched GEMM)
+* The GCN stack in eval mode (no autograd) takes the concatenation-free path (forced on here; by default on
+  planes of >= models.FUSED_MIN_PLANE pixels); its output matches the unfused (cat kernel + batched GEMM)
   path to fp32 GEMM rounding.
 * Both workgroup shapes: BM = 256 output channels (C % 256 == 0) and BM = 128 (C = 128, 384).
 """
