@@ -129,6 +129,10 @@ def main():
             sweep("bwd", name, bwd_time, {"bwd_complete_mfma": [1], "bwd_mfma_cpw": [1, 2]})
         sweep("bwd", "cfg4", bwd_time, {"bwd_regular_mfma": [1], "bwd_mfma_cpw": [1, 2]})
         return
+    if what == "smallcap":  # 8x8-plane backward: channels per workgroup
+        for name in ("cfg3", "cfg2"):
+            sweep("bwd", name, bwd_time, {"bwd_fused_cap": [8, 16, 32, 64], "bwd_pre2": [0, 1]})
+        return
     if what == "smallbwd":  # 8x8-plane backward geometry (configs[2] / [3])
         for name in ("cfg3", "cfg2"):
             sweep("bwd", name, bwd_time, {"bwd_fused_lo": [4, 8, 16], "bwd_fused_hi": [8, 16],
