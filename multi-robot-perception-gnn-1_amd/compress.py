@@ -173,3 +173,59 @@ def compress_dual(conv: torch.nn.Conv2d, x: torch.Tensor, agg: torch.Tensor):
     _lib.check(code, "mrp_compress_dual_fwd")
     return y
 
+
+
+class FilmCompressFunction(torch.autograd.Function):
+    """``conv(torch.cat((x, film_mean(x, gb)), 1))`` (``models.py:181-184``) with autograd and without
+    the concatenation: forward = the aggregation kernel into its own (N, C, H, W) output, then the
+    two-source MFMA compress (``mrp_compress_dual_fwd``) reading x and the aggregate in place.
+    Backward: ``d cat = W^T dy`` (one batched GEMM into an (N, 2C, H, W) buffer, as the cat path's),
+    then ONE aggregation-backward pass with the first half as the base of x's gradient (so x's two
+    gradient terms are never added by a separate kernel), and the weight gradient as two half-width
+    GEMMs (x and the aggregate are separate tensors here).  Saves, per layer, the concatenation's
+    second copy of x (written by the cat kernel, read by the GEMM) and keeps the aggregate instead of
+    the 2C-channel buffer for backward."""
+
+    @staticmethod
+    def forward(ctx, x, gb, weight, bias, conv, csr, mode: int):
+        from .aggregate import film_mean_forward_into
+        agg = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+        film_mean_forward_into(x, gb, csr, mode, agg)
+        y = compress_dual(conv, x, agg)
+        if y is None:
+            raise RuntimeError("mrp_compress_dual_fwd does not cover this shape (callers check "
+                               "dual_compress_supported first)")
+        ctx.save_for_backward(x, gb, agg, weight)
+        ctx.csr, ctx.mode, ctx.has_bias = csr, mode, bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .aggregate import film_mean_backward
+        x, gb, agg, weight = ctx.saved_tensors
+        n, C, H, W = x.shape
+        gy = gy.contiguous()
+        need_x, need_gb = ctx.needs_input_grad[0], gb is not None and ctx.needs_input_grad[1]
+        dx = dgb = dw = db = None
+        if need_x or need_gb:
+            dcat = torch.bmm(weight.reshape(C, 2 * C).t().expand(n, 2 * C, C), gy.view(n, C, H * W))
+            dcat = dcat.view(n, 2 * C, H, W)
+            dx, dgb = film_mean_backward(dcat[:, C:], x, gb, ctx.csr, ctx.mode, need_x, need_gb,
+                                         grad_x_base=dcat[:, :C] if need_x else None)
+            if dgb is not None:
+                dgb = dgb.view(gb.shape).to(gb.dtype)
+        if ctx.needs_input_grad[2]:
+            half = (C, C, 1, 1)
+            dw = torch.cat((torch.nn.grad.conv2d_weight(x, half, gy),
+                            torch.nn.grad.conv2d_weight(agg, half, gy)), 1)
+        if ctx.has_bias and ctx.needs_input_grad[3]:
+            db = gy.sum((0, 2, 3))
+        return dx, dgb, dw, db, None, None, None
+
+
+def film_compress(conv: torch.nn.Conv2d, x: torch.Tensor, gb, csr, mode: int) -> torch.Tensor:
+    """Autograd form of ``conv(torch.cat((x, film_mean(x, gb)), 1))`` without the concatenation
+    (``FilmCompressFunction``); the caller checks ``dual_compress_supported(conv, x)``."""
+    if gb is not None:
+        gb = gb.reshape(csr.num_edges, x.shape[1], 2)
+    return FilmCompressFunction.apply(x, gb, conv.weight, conv.bias, conv, csr, mode)

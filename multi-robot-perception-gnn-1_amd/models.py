@@ -34,7 +34,7 @@ import torch
 import torch.nn as nn
 
 from .aggregate import film_mean, film_mean_cat, film_mean_mix, film_mean_residual
-from .compress import (compress_1x1, compress_dual, compress_film_fused, dual_compress_supported,
+from .compress import (compress_1x1, compress_dual, compress_film_fused, dual_compress_supported, film_compress,
                        fused_compress_supported)
 from .encoder import edge_logits
 
@@ -135,7 +135,8 @@ class GCN(nn.Module):
         (eval, ``test_dgl``), on the planes where it measured faster (``set_fused_compress``), the
         concatenation is never written: the aggregate kernel, then the two-source MFMA compress
         (``mrp_compress_dual_fwd``), or the single fused kernel (``mrp_compress_film_fwd``) in
-        "fused" mode; otherwise (and with autograd) the cat kernel + batched GEMM."""
+        "fused" mode; with autograd on those planes the same two-source forward with its own backward
+        (``FilmCompressFunction``); otherwise the cat kernel + batched GEMM."""
         x = feats
         setting = fused_compress_setting()
         if (x.is_cuda and self._return_mode() != "input" and not torch.is_grad_enabled()
@@ -152,6 +153,15 @@ class GCN(nn.Module):
                 y = compress_dual(conv, x, self(g, x))
                 if y is not None:
                     return y
+        if (x.is_cuda and torch.is_grad_enabled() and self._return_mode() != "input"
+                and setting != "fused" and fused_compress_enabled(x.shape[-2] * x.shape[-1])
+                and dual_compress_supported(conv, x)):
+            # training: the same concatenation-free forward with its own backward (FilmCompressFunction)
+            mode = _opt(self.opt, "gcn_mode", "film_mean")
+            if mode == "copy_mean":
+                return film_compress(conv, x, None, g.csr(x.device), _lib_modes()[mode])
+            z = self.edge_encoder.logits(g.edata["pose"])
+            return film_compress(conv, x, z, g.csr(x.device), _lib_modes()[mode] | _lib_logits())
         return compress_1x1(conv, self.forward_cat(g, x))
 
     def forward_residual(self, g, feats: torch.Tensor = None) -> torch.Tensor:
