@@ -135,8 +135,9 @@ class GCN(nn.Module):
         (eval, ``test_dgl``), on the planes where it measured faster (``set_fused_compress``), the
         concatenation is never written: the aggregate kernel, then the two-source MFMA compress
         (``mrp_compress_dual_fwd``), or the single fused kernel (``mrp_compress_film_fwd``) in
-        "fused" mode; with autograd on those planes the same two-source forward with its own backward
-        (``FilmCompressFunction``); otherwise the cat kernel + batched GEMM."""
+        "fused" mode; otherwise (and with autograd) the cat kernel + batched GEMM, or, opted in with
+        ``set_training_compress(True)``, the two-source forward with its own backward
+        (``FilmCompressFunction``)."""
         x = feats
         setting = fused_compress_setting()
         if (x.is_cuda and self._return_mode() != "input" and not torch.is_grad_enabled()
@@ -153,10 +154,10 @@ class GCN(nn.Module):
                 y = compress_dual(conv, x, self(g, x))
                 if y is not None:
                     return y
-        if (x.is_cuda and torch.is_grad_enabled() and self._return_mode() != "input"
-                and setting != "fused" and fused_compress_enabled(x.shape[-2] * x.shape[-1])
+        if (_TRAIN_DUAL[0] and x.is_cuda and torch.is_grad_enabled() and self._return_mode() != "input"
                 and dual_compress_supported(conv, x)):
-            # training: the same concatenation-free forward with its own backward (FilmCompressFunction)
+            # opt-in training path: the concatenation-free forward with its own backward
+            # (FilmCompressFunction; set_training_compress)
             mode = _opt(self.opt, "gcn_mode", "film_mean")
             if mode == "copy_mean":
                 return film_compress(conv, x, None, g.csr(x.device), _lib_modes()[mode])
@@ -196,6 +197,19 @@ _FUSED_COMPRESS = ["auto"]
 # (configs[2] 0.85 vs 0.81 ms, [3] 0.54 vs 0.51 ms) the cat kernel + library GEMM stays
 # (tools/exp_compress_dual.py, both paths timed alternately on the same box)
 FUSED_MIN_PLANE = 1024
+
+
+# Training through FilmCompressFunction (no concatenation; backward: W^T dy, one aggregation-backward
+# pass, two half-width weight-gradient GEMMs).  Off: at configs[1] the step measured 8.18 ms either
+# way (tools/exp_train_dual.py) — the forward's saving is spent on the two half-width MIOpen weight
+# gradients and their layout transposes (2.36 + 0.78 ms against 2.13 + 0.62 ms for one full call).
+_TRAIN_DUAL = [False]
+
+
+def set_training_compress(enabled: bool) -> None:
+    """Opt the autograd (training) GCN layer into the concatenation-free compress (True) or keep
+    the cat kernel + batched GEMM (False, default)."""
+    _TRAIN_DUAL[0] = bool(enabled)
 
 
 def fused_compress_enabled(plane: int = None) -> bool:

@@ -210,10 +210,10 @@ def test_stack_eval_fused_mode(cuda_device):
 
 @pytest.mark.parametrize("B,N,C,H", [(3, 8, 256, 8), (2, 5, 128, 16), (2, 8, 128, 32)])
 def test_training_concatenation_free_layer(cuda_device, B, N, C, H):
-    """With autograd, set_fused_compress(True) trains through FilmCompressFunction (aggregate kernel +
-    two-source GEMM forward; W^T dy, one aggregation-backward pass with the x half as its base, two
-    half-width weight-gradient GEMMs): the loss, the input gradient and every parameter gradient
-    agree with the cat kernel + batched GEMM path to fp32 GEMM rounding."""
+    """With autograd and set_training_compress(True) the layer trains through FilmCompressFunction
+    (aggregate kernel + two-source GEMM forward; W^T dy, one aggregation-backward pass with the x half
+    as its base, two half-width weight-gradient GEMMs): the output, the input gradient and every
+    parameter gradient agree with the cat kernel + batched GEMM path to fp32 GEMM rounding."""
     opt = types.SimpleNamespace(feature_dim=C, compress_gcn=True, multi_gcn=True)
     torch.manual_seed(5)
     net = m.GCNBlock(opt).to(cuda_device)
@@ -221,17 +221,16 @@ def test_training_concatenation_free_layer(cuda_device, B, N, C, H):
     x0 = g.ndata["image"]
     G = torch.randn_like(x0)
     res = []
-    prev = m.models.fused_compress_setting()
     try:
         for setting in (True, False):
-            m.models.set_fused_compress(setting)
+            m.models.set_training_compress(setting)
             net.zero_grad()
             x = x0.clone().requires_grad_(True)
             y = net(g, x)
             (y * G).sum().backward()
             res.append((y.detach(), x.grad, {k: p.grad.clone() for k, p in net.named_parameters()}))
     finally:
-        m.models.set_fused_compress(prev)
+        m.models.set_training_compress(False)
     (ya, dxa, pa), (yb, dxb, pb) = res
 
     def rel(a, b):
