@@ -128,7 +128,7 @@ struct Lds {
 // One K stage (16 input channels, both halves) of a consumer wave's 32 x (NT x 16) output block:
 // W fragments from the k4-packed image (narrow or wide reads, kWideA), x / aggregate fragments from
 // the [node][channel][pixel] images (kPackB: k4-packed instead).
-template <int NT, int BM>
+template <int NT, int BM, bool WIDEA = kWideA>
 __device__ __forceinline__ void consume_stage(f32x4 (&acc)[2][NT], const float* Xs, const float* As, const float* Ws,
                                               int w, int lk, int lc) {
 #pragma unroll
@@ -136,7 +136,7 @@ __device__ __forceinline__ void consume_stage(f32x4 (&acc)[2][NT], const float* 
     const f4* B4 = reinterpret_cast<const f4*>(h == 0 ? Xs : As);
     const f4* A4 = reinterpret_cast<const f4*>(Ws);
     f4 af[2], bf[NT];
-    if (kWideA) {
+    if (WIDEA) {
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb) af[mb] = A4[(h * 4 + lk) * BM + 32 * w + 16 * mb + lc];
     } else {
@@ -459,6 +459,7 @@ struct DualArgs {
   int32_t C, P, num_nodes, ntiles_p, ntiles_m, remap;
 };
 
+template <bool WIDEA>
 __global__ void __launch_bounds__(Geo<4>::THREADS) compress_dual_fwd(DualArgs a) {
   constexpr int NT = 8, NC = 4;
   using L = Lds<NT, NC>;
@@ -528,7 +529,7 @@ __global__ void __launch_bounds__(Geo<4>::THREADS) compress_dual_fwd(DualArgs a)
   for (int s = 0; s < nstages; ++s) {
     __syncthreads();
     const float* Xs = smem + (s & 1) * L::BUF;
-    consume_stage<NT, BM>(acc, Xs, Xs + L::XS, Xs + 2 * L::XS, w, lk, lc);
+    consume_stage<NT, BM, WIDEA>(acc, Xs, Xs + L::XS, Xs + 2 * L::XS, w, lk, lc);
   }
   store_tile<NT, BM>(acc, a.y, a.ys, a.bias, a.P, m0, p0, node0, nvalid, w, lk, lc);
 }
@@ -659,11 +660,17 @@ extern "C" int mrp_compress_dual_fwd(const float* x, int64_t x_node_stride, cons
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   a.remap = grid % 8 == 0 ? 1 : 0;
   const size_t lds = (size_t)mrp_cf::Lds<8, 4>::TOTAL * sizeof(float);
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&mrp_cf::compress_dual_fwd),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL(mrp_cf::compress_dual_fwd, dim3((unsigned)grid), dim3(mrp_cf::Geo<4>::THREADS), lds,
-                     static_cast<hipStream_t>(stream), a);
+  // W fragments as four ds_read_b32 (default) or, lab hook bit 128, one ds_read_b128 per k4 set:
+  // 1056 vs 1049 us at configs[1] and 0.5-1 % slower at every other config (tools/exp_compress_dual.py)
+  const bool wide = (mrp_cf_debug & 128) != 0;
+  auto* kern = wide ? &mrp_cf::compress_dual_fwd<true> : &mrp_cf::compress_dual_fwd<false>;
+  static const hipError_t attr_w = hipFuncSetAttribute(reinterpret_cast<const void*>(&mrp_cf::compress_dual_fwd<true>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static const hipError_t attr_n = hipFuncSetAttribute(reinterpret_cast<const void*>(&mrp_cf::compress_dual_fwd<false>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr_w != hipSuccess) return attr_w;
+  if (attr_n != hipSuccess) return attr_n;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(mrp_cf::Geo<4>::THREADS), lds, static_cast<hipStream_t>(stream), a);
   return hipGetLastError();
 }
 

@@ -30,7 +30,13 @@ for name, (B, N, C, H, knn) in SHAPES.items():
         t_gemm = time_launches([lambda: compress_1x1(conv, cat)], 20, dev)
         t_agg = time_launches([lambda: mrp.film_mean_forward_into(x, z, csr, MODE, agg)], 20, dev)
         t_dual = time_launches([lambda: compress_dual(conv, x, agg)], 20, dev)
+        lib = mrp.load_library()
+        lib.mrp_compress_film_debug(128)  # W fragments by ds_read_b128 (the four-b32 form is the default)
+        t_wide = time_launches([lambda: compress_dual(conv, x, agg)], 20, dev)
+        lib.mrp_compress_film_debug(0)
         flop = 2 * x.shape[0] * H * H * C * 2 * C
+        print(f"{name}: dual GEMM narrow-A {t_dual * 1e6:7.1f} us ({flop / t_dual / 1e12:5.1f} TF/s), "
+              f"wide-A {t_wide * 1e6:7.1f} us ({flop / t_wide / 1e12:5.1f} TF/s)", flush=True)
         print(f"{name}: cat {t_cat * 1e6:7.1f} + library GEMM {t_gemm * 1e6:7.1f} us ({flop / t_gemm / 1e12:5.1f} TF/s)"
               f" = {(t_cat + t_gemm) * 1e6:7.1f} us | aggregate {t_agg * 1e6:7.1f} + dual {t_dual * 1e6:7.1f} us "
               f"({flop / t_dual / 1e12:5.1f} TF/s) = {(t_agg + t_dual) * 1e6:7.1f} us", flush=True)
