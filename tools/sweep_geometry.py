@@ -129,6 +129,8 @@ def main():
             sweep("bwd", name, bwd_time, {"bwd_complete_mfma": [1], "bwd_mfma_cpw": [1, 2]})
         sweep("bwd", "cfg4", bwd_time, {"bwd_regular_mfma": [1], "bwd_mfma_cpw": [1, 2]})
         return
+    # "gramparts" (removed with its kernel hooks): film_bwd_fused at configs[3] with the lane reduction,
+    # the d gamma/beta stores or the Gram FMAs skipped: 25.2 us -> 23.3 / 23.2 / 23.1, all three 21.0
     if what == "smallcap":  # 8x8-plane backward: channels per workgroup
         for name in ("cfg3", "cfg2"):
             sweep("bwd", name, bwd_time, {"bwd_fused_cap": [8, 16, 32, 64], "bwd_pre2": [0, 1]})
