@@ -1,5 +1,5 @@
 #pragma once
-// film_mean.hip — gfx950 (MI355X / CDNA4) kernels for the FiLM-mean GCN aggregation.
+// film_mean_kernels.hpp — gfx950 (MI355X / CDNA4) kernels for the FiLM-mean GCN aggregation
 //
 // Hot path replaced (xjh19971/multi-robot-perception-gnn-1):
 //   GCN.forward                      dgl/model/models.py:219-226
