@@ -1518,62 +1518,33 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
   float s = a.mode != MRP_AGG_FILM_SUM && K > 0 ? 1.f / (float)K : 1.f;
   s *= a.agg_scale;  // epilogue: grad_out reaches the aggregate scaled
 
-  // ---- prologue: thread t owns (channel t % CPB, destination t / CPB): column v of that channel's
-  // Wt (and, REGULAR, channel 0: v's slot row).  Index loads first, gamma after.
-  for (int t = threadIdx.x; t < CPB * NPB; t += blockDim.x) {
-    const int cl = t % CPB, v = t / CPB;
-    const bool ok = v < n && c0 + cl < a.C;
-    constexpr int NE = COMPLETE ? NPB : KMAX;  // candidate in-edges of v
-    int us[NE];
-    int64_t es[NE];
+  // ---- prologue: thread t < CPB NPB owns (channel t % CPB, destination t / CPB): column v of that
+  // channel's Wt (and, REGULAR, channel 0: v's slot row).  Order (vmcnt retires in issue order):
+  // index loads, then the wave's first pixel group, then gamma (needs the edge ids) — so the two
+  // dependent prologue round trips run under the first group's loads instead of before them.
+  static_assert(CPB * NPB <= kBlock, "one prologue item per thread");
+  constexpr int NE = COMPLETE ? NPB : KMAX;  // candidate in-edges of v
+  const int pt = threadIdx.x;
+  const bool pitem = pt < CPB * NPB;
+  const int pcl = pt % CPB, pv = pt / CPB;
+  int us[NE];
+  int64_t es[NE];
+  {
+    const bool ok = pitem && pv < n && c0 + pcl < a.C;
 #pragma unroll
     for (int jj = 0; jj < NE; ++jj) {
       if (COMPLETE) {
-        const bool on = ok && jj < n && jj != v;
+        const bool on = ok && jj < n && jj != pv;
         us[jj] = on ? jj : -1;
-        es[jj] = on ? complete_eid(ebase, n, jj, v) : -1;
+        es[jj] = on ? complete_eid(ebase, n, jj, pv) : -1;
       } else {
         const bool on = ok && jj < K;
-        const int k = (node0 + (on ? v : 0)) * K + (on ? jj : 0);
+        const int k = (node0 + (on ? pv : 0)) * K + (on ? jj : 0);
         us[jj] = on ? a.src[k] - node0 : -1;
         es[jj] = on ? a.eid[k] : -1;
       }
     }
-    float gm[NE];
-#pragma unroll
-    for (int jj = 0; jj < NE; ++jj) {
-      gm[jj] = 0.f;
-      if (es[jj] >= 0) {
-        if (a.mode == MRP_AGG_COPY_MEAN) {
-          gm[jj] = 1.f;
-        } else {
-          gm[jj] = a.gb[(es[jj] * a.C + c0 + cl) * 2];
-          if (a.logits) gm[jj] = sigmoidf(gm[jj]);
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < NPB; ++u) {
-      float wv = 0.f;
-      if (COMPLETE) {
-        wv = s * gm[u];
-      } else {
-#pragma unroll
-        for (int jj = 0; jj < NE; ++jj)  // += in slot order: multi-edges sum like the CSR tile build
-          if (us[jj] == u) wv += s * gm[jj];
-      }
-      Wt[(cl * NPB + u) * WR + v] = wv;
-    }
-    if (!COMPLETE && cl == 0) {
-#pragma unroll
-      for (int jj = 0; jj < KMAX; ++jj) {
-        const bool in = (unsigned)us[jj] < (unsigned)n;  // outside the graph: rejected on the host
-        slot_u[v * KMAX + jj] = in ? us[jj] : 0;
-        slot_e[v * KMAX + jj] = in ? (int)es[jj] : -1;
-      }
-    }
   }
-  __syncthreads();
 
   // 16-row index vn -> (channel of the pair, node).  This lane's G rows: vn = 4q + bb; its x row: jl.
   uint32_t goff4[4], boff4[4], ooff4[4];
@@ -1622,6 +1593,44 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
             reinterpret_cast<const mf4*>(at_bytes(xbase, xo + (uint32_t)g * 256u + (uint32_t)t * 64u)));
     }
   };
+
+  if (nsteps > 0) load_step(0, gq, xn);  // the first pixel group, ahead of the gamma loads
+  if (pitem) {
+    float gm[NE];
+#pragma unroll
+    for (int jj = 0; jj < NE; ++jj) {
+      gm[jj] = 0.f;
+      if (es[jj] >= 0) {
+        if (a.mode == MRP_AGG_COPY_MEAN) {
+          gm[jj] = 1.f;
+        } else {
+          gm[jj] = a.gb[(es[jj] * a.C + c0 + pcl) * 2];
+          if (a.logits) gm[jj] = sigmoidf(gm[jj]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NPB; ++u) {
+      float wv = 0.f;
+      if (COMPLETE) {
+        wv = s * gm[u];
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < NE; ++jj)  // += in slot order: multi-edges sum like the CSR tile build
+          if (us[jj] == u) wv += s * gm[jj];
+      }
+      Wt[(pcl * NPB + u) * WR + pv] = wv;
+    }
+    if (!COMPLETE && pcl == 0) {
+#pragma unroll
+      for (int jj = 0; jj < KMAX; ++jj) {
+        const bool in = (unsigned)us[jj] < (unsigned)n;  // outside the graph: rejected on the host
+        slot_u[pv * KMAX + jj] = in ? us[jj] : 0;
+        slot_e[pv * KMAX + jj] = in ? (int)es[jj] : -1;
+      }
+    }
+  }
+  __syncthreads();
 
   float wa[4];
   mf4 dacc = {0.f, 0.f, 0.f, 0.f};  // Gram: D[4q + r][jl] of the current block
@@ -1705,8 +1714,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
   };
 
   // software pipeline over the wave's (block, pixel group) steps: two register sets, the next step's
-  // loads in flight under the current step's MFMAs
-  if (nsteps > 0) load_step(0, gq, xn);
+  // loads in flight under the current step's MFMAs (step 0 was issued in the prologue)
   for (int st = 0; st < nsteps; st += 2) {
     if (st + 1 < nsteps) load_step(st + 1, gq2, xn2);
     compute_step(st, gq, xn);
