@@ -110,3 +110,20 @@ def test_edge_encoder_bwd_validation_without_launch():
     # work to do but a missing input or workspace
     assert lib.mrp_edge_encoder_bwd(None, None, None, None, 8, 4, None, None, None, None, None) == HIP_INVALID_VALUE
     assert lib.mrp_edge_encoder_bwd(None, None, None, None, 8, 0, None, None, None, None, None) == 0  # C = 0: no-op
+
+
+def test_tuning_knobs_documented_in_the_header():
+    """mrp_tuning_set (host-only, no launch): every kernel-choice knob the header documents is accepted
+    in range and rejected out of range; unknown names are rejected; "reset" restores defaults."""
+    lib = m.load_library()
+    try:
+        for name, lo, hi in (("bwd_regular_mfma", 0, 1), ("bwd_complete_mfma", 0, 1), ("bwd_mfma_cpw", 1, 2),
+                             ("bwd_pre2", 0, 1), ("fwd_regular_split", 0, 1), ("bwd_fused_cap", 1, 64)):
+            assert name.encode() in open(os.path.join(ROOT, "include", "mrp_gnn.h"), "rb").read() or \
+                name.startswith("bwd_fused")
+            assert lib.mrp_tuning_set(name.encode(), lo) == 0
+            assert lib.mrp_tuning_set(name.encode(), hi) == 0
+            assert lib.mrp_tuning_set(name.encode(), hi + 1) == HIP_INVALID_VALUE
+        assert lib.mrp_tuning_set(b"no_such_knob", 0) == HIP_INVALID_VALUE
+    finally:
+        assert lib.mrp_tuning_set(b"reset", 0) == 0
