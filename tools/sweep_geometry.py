@@ -131,6 +131,10 @@ def main():
         return
     # "gramparts" (removed with its kernel hooks): film_bwd_fused at configs[3] with the lane reduction,
     # the d gamma/beta stores or the Gram FMAs skipped: 25.2 us -> 23.3 / 23.2 / 23.1, all three 21.0
+    if what == "bigbwd1":  # 32x32 backward with one slice per lane (a plane over 4 waves)
+        for name in ("cfg1", "north_star"):
+            sweep("bwd", name, bwd_time, {"bwd_fused_lo": [128, 256], "bwd_fused_hi": [256], "bwd_fused_cap": [1]})
+        return
     if what == "bigbwd":  # 32x32-plane backward geometry (headline / configs[1])
         for name in ("cfg1",):
             sweep("bwd", name, bwd_time, {"bwd_fused_lo": [32, 64, 128], "bwd_fused_hi": [64, 128, 256],
