@@ -5,7 +5,11 @@ A 1x1 convolution over NCHW is, per node n, ``Y_n = W X_n + b`` with W (C, 2C) s
 node's (2C, H*W) block — a strided-batched GEMM with a broadcast A operand.  Measured on MI355X
 (``tools/exp_compress*.py``): at Nt=256, C=512, 32x32 the batched GEMM takes 2159 us forward and
 2012 us for the input gradient against 2674 / 2363 us for MIOpen's convolution (127 vs 106 TF/s of
-the 157 TF/s fp32 MFMA peak); the weight gradient stays MIOpen's (no (Nt, C, 2C) temporary).
+the 157 TF/s fp32 MFMA peak).  The weight gradient ``dW = sum_n dy_n h_n^T`` is a batched GEMM into an
+(Nt, C, 2C) temporary + a sum over nodes on planes of >= 1024 pixels (configs[1] 1.04 vs 1.27 ms,
+headline size 2.06 vs 2.55 ms for MIOpen's, whose NCHW -> NHWC transposes it skips), MIOpen's
+convolution weight gradient on smaller planes, where its K = H W GEMMs are too short
+(``tools/exp_compress_wgrad.py``: configs[2] 1.06 vs 1.88 ms, [3] 0.54 vs 1.26, [4] 1.12 vs 1.30).
 Same fp32 arithmetic as the convolution, different summation order: ≤ 1e-5 relative.
 The module keeps the reference's ``nn.Conv2d`` parameters (``conv1.weight`` (C, 2C, 1, 1),
 ``conv1.bias``), so ``state_dict`` keys are unchanged.
@@ -17,6 +21,22 @@ import ctypes
 import torch
 
 from . import _lib
+
+
+# the batched-GEMM weight gradient: planes of at least this many pixels, temporaries up to this size
+WGRAD_BMM_MIN_PLANE = 1024
+WGRAD_BMM_MAX_TEMP = 1 << 30
+
+
+def weight_grad_1x1(h: torch.Tensor, wshape, gy: torch.Tensor) -> torch.Tensor:
+    """``torch.nn.grad.conv2d_weight(h, wshape, gy)`` for a 1x1 conv over (N, K, H, W) input h and
+    (N, C, H, W) output gradient gy (both contiguous fp32), by the faster route for the plane size."""
+    n, k, H, W = h.shape
+    c = wshape[0]
+    P = H * W
+    if P >= WGRAD_BMM_MIN_PLANE and n * c * k * 4 <= WGRAD_BMM_MAX_TEMP:
+        return torch.bmm(gy.reshape(n, c, P), h.reshape(n, k, P).transpose(1, 2)).sum(0).view(wshape)
+    return torch.nn.grad.conv2d_weight(h, wshape, gy)
 
 
 class Compress1x1Function(torch.autograd.Function):
@@ -45,7 +65,7 @@ class Compress1x1Function(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dh = torch.bmm(weight.reshape(c, k).t().expand(n, k, c), gy.view(n, c, H * W)).view(n, k, H, W)
         if ctx.needs_input_grad[1]:
-            dw = torch.nn.grad.conv2d_weight(h, weight.shape, gy)
+            dw = weight_grad_1x1(h, weight.shape, gy)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = gy.sum((0, 2, 3))
         return dh, dw, db
@@ -216,8 +236,7 @@ class FilmCompressFunction(torch.autograd.Function):
                 dgb = dgb.view(gb.shape).to(gb.dtype)
         if ctx.needs_input_grad[2]:
             half = (C, C, 1, 1)
-            dw = torch.cat((torch.nn.grad.conv2d_weight(x, half, gy),
-                            torch.nn.grad.conv2d_weight(agg, half, gy)), 1)
+            dw = torch.cat((weight_grad_1x1(x.contiguous(), half, gy), weight_grad_1x1(agg, half, gy)), 1)
         if ctx.has_bias and ctx.needs_input_grad[3]:
             db = gy.sum((0, 2, 3))
         return dx, dgb, dw, db, None, None, None
