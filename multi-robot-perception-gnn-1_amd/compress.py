@@ -5,11 +5,12 @@ A 1x1 convolution over NCHW is, per node n, ``Y_n = W X_n + b`` with W (C, 2C) s
 node's (2C, H*W) block — a strided-batched GEMM with a broadcast A operand.  Measured on MI355X
 (``tools/exp_compress*.py``): at Nt=256, C=512, 32x32 the batched GEMM takes 2159 us forward and
 2012 us for the input gradient against 2674 / 2363 us for MIOpen's convolution (127 vs 106 TF/s of
-the 157 TF/s fp32 MFMA peak).  The weight gradient ``dW = sum_n dy_n h_n^T`` is a batched GEMM into an
-(Nt, C, 2C) temporary + a sum over nodes on planes of >= 1024 pixels (configs[1] 1.04 vs 1.27 ms,
-headline size 2.06 vs 2.55 ms for MIOpen's, whose NCHW -> NHWC transposes it skips), MIOpen's
-convolution weight gradient on smaller planes, where its K = H W GEMMs are too short
-(``tools/exp_compress_wgrad.py``: configs[2] 1.06 vs 1.88 ms, [3] 0.54 vs 1.26, [4] 1.12 vs 1.30).
+the 157 TF/s fp32 MFMA peak).  The weight gradient ``dW = sum_n dy_n h_n^T`` (``weight_grad_1x1``,
+``tools/exp_compress_wgrad.py``, against MIOpen's weight-gradient convolution with its NCHW -> NHWC
+transposes): on planes of >= 1024 pixels a batched GEMM into an (Nt, C, 2C) temporary + a sum over
+nodes (configs[1] 1.04 vs 1.28 ms, headline size 2.06 vs 2.60 ms); on smaller planes, where K = H W
+is too short for that, channel-major copies of dy and h and ONE GEMM with K = Nt H W (configs[2]
+0.96 vs 1.06 ms, [3] 0.51 vs 0.54, [4] 1.07 vs 1.12).
 Same fp32 arithmetic as the convolution, different summation order: ≤ 1e-5 relative.
 The module keeps the reference's ``nn.Conv2d`` parameters (``conv1.weight`` (C, 2C, 1, 1),
 ``conv1.bias``), so ``state_dict`` keys are unchanged.
@@ -36,7 +37,9 @@ def weight_grad_1x1(h: torch.Tensor, wshape, gy: torch.Tensor) -> torch.Tensor:
     P = H * W
     if P >= WGRAD_BMM_MIN_PLANE and n * c * k * 4 <= WGRAD_BMM_MAX_TEMP:
         return torch.bmm(gy.reshape(n, c, P), h.reshape(n, k, P).transpose(1, 2)).sum(0).view(wshape)
-    return torch.nn.grad.conv2d_weight(h, wshape, gy)
+    a = gy.reshape(n, c, P).permute(1, 0, 2).reshape(c, n * P)
+    bt = h.reshape(n, k, P).permute(1, 0, 2).reshape(k, n * P)
+    return torch.mm(a, bt.t()).view(wshape)
 
 
 class Compress1x1Function(torch.autograd.Function):

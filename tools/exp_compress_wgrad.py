@@ -39,15 +39,23 @@ def main():
         def bmm_sum():
             return torch.bmm(dy.view(Nt, C, P), h.view(Nt, 2 * C, P).transpose(1, 2)).sum(0).view(wshape)
 
+        def perm_mm():  # channel-major copies of dy and h, then one GEMM with K = Nt P
+            a = dy.view(Nt, C, P).permute(1, 0, 2).reshape(C, Nt * P)
+            bt = h.view(Nt, 2 * C, P).permute(1, 0, 2).reshape(2 * C, Nt * P)
+            return torch.mm(a, bt.t()).view(wshape)
+
         ref = miopen().double()
         err = float((bmm_sum().double() - ref).abs().max() / ref.abs().max())
-        ta, tb = [], []
+        err2 = float((perm_mm().double() - ref).abs().max() / ref.abs().max())
+        ta, tb, tc = [], [], []
         for _ in range(3):
             ta.append(timeit(miopen))
             tb.append(timeit(bmm_sum))
-        ta, tb = sorted(ta)[1], sorted(tb)[1]
+            tc.append(timeit(perm_mm))
+        ta, tb, tc = sorted(ta)[1], sorted(tb)[1], sorted(tc)[1]
         print(f"{name:10s} Nt={Nt} C={C} P={P}: MIOpen wgrad {ta:.3f} ms, bmm + sum {tb:.3f} ms "
-              f"(temp {Nt * C * 2 * C * 4 / 2**20:.0f} MiB), rel diff {err:.1e}", flush=True)
+              f"(temp {Nt * C * 2 * C * 4 / 2**20:.0f} MiB, rel diff {err:.1e}), permute copies + mm {tc:.3f} ms "
+              f"(rel diff {err2:.1e})", flush=True)
         del h, dy
         torch.cuda.empty_cache()
 
