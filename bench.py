@@ -304,44 +304,19 @@ def config_record(cid, world, rank, device, args):
     rec = {"config": cfg["name"], "graphs_per_rank": hi - lo, "share": share, "robots": N, "channels": C,
            "H": H, "W": H, "layers": layers, "graph": f"k-NN({knn})" if knn else "complete",
            "graph_kind": "regular" if knn else "complete", "scaling": scaling}
-    # the eval forward (models.py's compress policy) and, for comparison, the other compress path:
-    # timed alternately, three rounds each, median per path — the first timed block of a sequence
-    # runs a few % slow (clocks), which a single A-then-B comparison would credit to the path
-    fused = (mrp.models.fused_compress_enabled(P)
-             and mrp.compress.dual_compress_supported(net.conv1, x))
-    prev = mrp.models.fused_compress_setting()
-    fwd = lambda: net(g, x)  # noqa: E731
-    ts, ts_other = [], []
-    try:
-        with torch.no_grad():
-            for _ in range(3):
-                fwd()
-            for _ in range(3):
-                for other in (False, True):
-                    mrp.models.set_fused_compress(prev if not other else (not fused))
-                    for _ in range(2):
-                        fwd()
-                    (ts_other if other else ts).append(timed(fwd, args.config_steps, world, device,
-                                                             args.dist_backend))
-    finally:
-        mrp.models.set_fused_compress(prev)
-    t, t_other = sorted(ts)[1], sorted(ts_other)[1]
-    rec["forward"] = {"value": world * elems / t if scaling == "weak" else None, "unit": "elems/s",
-                      "ms_per_step": t * 1e3}
-    rec["forward"]["compress"] = ("aggregate kernel + two-source MFMA compress (no cat buffer)" if fused
-                                  else "cat kernel + library GEMM")
-    rec["forward"]["ms_per_step_other_compress"] = t_other * 1e3
-    if scaling == "strong":  # every rank holds a different part of one global batch
-        tot = torch.tensor([float(elems)], dtype=torch.float64,
-                           device=device if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(tot)
-        rec["forward"]["value"] = float(tot.item()) / t
-    # training step: forward + backward (+ RCCL gradient all-reduce, weighted by shard size)
+    # forward and training step on the matrix-core compress kernels ("hip", the product path) and, for
+    # comparison, on the cat kernel + torch's library GEMMs ("library", the round-2 path): timed
+    # alternately, three rounds each, median per path — the first timed block of a sequence runs a
+    # few % slow (clocks), which a single A-then-B comparison would credit to the path
     xr = x.detach().clone().requires_grad_(True)
     gy = torch.randn(Nt, C, H, H, device=device)
     reducer = GradAllReducer(net.parameters()) if world > 1 else None
     if reducer is not None:
         reducer.set_local_count(hi - lo)
+
+    def fwd():
+        with torch.no_grad():
+            net(g, x)
 
     def train():
         for p in net.parameters():
@@ -350,10 +325,34 @@ def config_record(cid, world, rank, device, args):
         if reducer is not None:
             reducer.synchronize()
 
-    for _ in range(2):
-        train()
-    tt = timed(train, args.config_steps, world, device, args.dist_backend)
+    prev = mrp.compress.compress_path()
+    times = {(k, path): [] for k in ("fwd", "train") for path in ("hip", "library")}
+    try:
+        for _ in range(2):
+            fwd()
+            train()
+        for _ in range(3):
+            for path in ("hip", "library"):
+                mrp.compress.set_compress_path(path)
+                for k, fn in (("fwd", fwd), ("train", train)):
+                    for _ in range(2):
+                        fn()
+                    times[(k, path)].append(timed(fn, args.config_steps, world, device, args.dist_backend))
+    finally:
+        mrp.compress.set_compress_path(prev)
+    med = {k: sorted(v)[1] for k, v in times.items()}
+    t, tt = med[("fwd", "hip")], med[("train", "hip")]
+    rec["forward"] = {"value": world * elems / t if scaling == "weak" else None, "unit": "elems/s",
+                      "ms_per_step": t * 1e3,
+                      "compress": "aggregate kernel + matrix-core compress kernel (no cat buffer)",
+                      "ms_per_step_library_compress": med[("fwd", "library")] * 1e3}
+    if scaling == "strong":  # every rank holds a different part of one global batch
+        tot = torch.tensor([float(elems)], dtype=torch.float64,
+                           device=device if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(tot)
+        rec["forward"]["value"] = float(tot.item()) / t
     rec["train_step"] = {"value": rec["forward"]["value"] * t / tt, "unit": "elems/s", "ms_per_step": tt * 1e3,
+                         "ms_per_step_library_compress": med[("train", "library")] * 1e3,
                          "allreduce": (f"{len(reducer.buckets)} bucket(s), {sum(p.numel() for p in net.parameters()) * 4 / 2**20:.1f} MiB"
                                        if reducer is not None else None)}
     if reducer is not None:

@@ -218,50 +218,34 @@ int64_t mrp_film_mean_bwd_workspace(int32_t num_graphs, int32_t max_nodes, int32
                                     int32_t C, int32_t P);
 
 /*
- * The layer's 1x1 compress convolution with the aggregation fused into it (dgl/model/models.py:181-184:
- * g_h = gcn1(g); h = conv1(torch.cat((h, g_h), 1))), forward, fp32 on the matrix cores:
+ * The layer's 1x1 compress convolution and its gradients, fp32 on the matrix cores (exact fp32
+ * products, v_mfma_f32_16x16x4_f32), without the concatenation (dgl/model/models.py:163-165,181-184,
+ * 186-189: h = conv(torch.cat((x, a), 1)) with conv = nn.Conv2d(2C, C, kernel_size=1)).  W is the
+ * conv weight (C, 2C) row-major (nn.Conv2d's (C, 2C, 1, 1)); x and a are the two halves of the
+ * concatenation as separate node-major tensors (any node strides, e.g. the two halves of one cat
+ * buffer).  Requirements (else hipErrorNotSupported): C % 32 == 0, P % 4 == 0, node strides % 4 == 0,
+ * every tensor 16-byte aligned, each operand's node range addressable with 31-bit byte offsets.
  *
- *   y[v, m, p] = sum_c W[m, c] x[v, c, p] + sum_c W[m, C + c] a[v, c, p] + bias[m]
- *
- * with a = the aggregate of mrp_film_mean_fwd (bit-identical), computed in the GEMM's operand
- * producer: the (N, 2C, P) concatenation is never written.  wt is the conv weight packed by
- * mrp_compress_weight_pack (2C^2 floats, 16-byte aligned); bias (C) may be NULL; y (num_nodes, C, P),
- * node stride y_node_stride.  Supports graph_kind MRP_GRAPH_COMPLETE with 2..8 nodes per graph,
- * P % 16 == 0, C % 128 == 0, (max_nodes - 1) x_node_stride + C P < 2^29 and C < 16384 (31-bit buffer
- * offsets); returns hipErrorNotSupported otherwise (run mrp_film_mean_cat_fwd + a GEMM).
+ * mrp_compress_fwd:       y[n] = W[:, :C] x[n] + W[:, C:] a[n] + bias      (bias (C) may be NULL)
+ * mrp_compress_bwd_data:  gx[n] = W[:, :C]^T gy[n],  ga[n] = W[:, C:]^T gy[n]
+ *                         wt = W^T (2C, C), from mrp_compress_weight_transpose
+ * mrp_compress_bwd_weight: gw = sum_n gy[n] [x[n]; a[n]]^T (C, 2C),  gbias = sum_{n,p} gy (may be
+ *                         NULL); split over the node-pixel axis into workspace (>=
+ *                         mrp_compress_bwd_weight_workspace bytes for the largest of the three node
+ *                         strides, 16-byte aligned; 0 = none needed), partial sums added in a fixed
+ *                         order (deterministic).  Also needs P % 32 == 0 and C % 8 == 0.
  */
-/*
- * Packs the 1x1 compress weight w (C, 2C) (nn.Conv2d(2C, C, 1).weight, row-major) into the layout
- * mrp_compress_film_fwd reads: wp[h][s][lk][m][k4] = w[m][h C + 16 s + 4 k4 + lk] (h < 2, s < C/16,
- * lk < 4, m < C, k4 < 4) — each 16-byte group is one MFMA lane's four k-steps of a 16-channel stage.
- * C % 16 == 0; wp 16-byte aligned, 2C^2 floats.  Run once per weight update.
- */
-int mrp_compress_weight_pack(const float* w, float* wp, int32_t C, void* stream);
-
-/*
- * The same compress from an aggregate already in HBM (mrp_film_mean_fwd's output):
- *   y[v, m, p] = sum_c W[m, c] x[v, c, p] + sum_c W[m, C + c] agg[v, c, p] + bias[m]
- * for any node count (nodes are tiled in groups of 8; no graph structure involved).  wt packed by
- * mrp_compress_weight_pack; operands staged by LDS-DMA.  C % 128 == 0, P % 16 == 0, x / agg / wt
- * 16-byte aligned with node strides multiples of 4 (else hipErrorNotSupported).
- */
-int mrp_compress_dual_fwd(const float* x, int64_t x_node_stride, const float* agg, int64_t agg_node_stride,
-                          int32_t num_nodes, int32_t C, int32_t P, const float* wt, const float* bias, float* y,
-                          int64_t y_node_stride, void* stream);
-
-int mrp_compress_film_fwd(const float* x, int64_t x_node_stride, const float* gb,
-                          int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
-                          int32_t num_nodes, int32_t num_edges, int32_t C, int32_t P, int32_t mode,
-                          const float* wt, const float* bias,
-                          float* y, int64_t y_node_stride, void* stream);
-
-/*
- * gb[i] = sigmoid(z[i]) for n floats (n % 4 == 0, 16-byte aligned), the expression the aggregation
- * kernels apply under MRP_AGG_GB_LOGITS, so a FiLM op fed gb without the flag gives the same bits as
- * one fed z with it.  Replaces the Sigmoid of the edge encoder, dgl/model/models.py:149.  Used ahead
- * of mrp_compress_film_fwd, whose workgroups would otherwise each re-evaluate the sigmoids.
- */
-int mrp_film_gate(const float* z, float* gb, int64_t n, void* stream);
+int mrp_compress_fwd(const float* x, int64_t x_node_stride, const float* a, int64_t a_node_stride,
+                     int32_t num_nodes, int32_t C, int32_t P, const float* w, const float* bias,
+                     float* y, int64_t y_node_stride, void* stream);
+int mrp_compress_weight_transpose(const float* w, float* wt, int32_t C, void* stream);
+int mrp_compress_bwd_data(const float* gy, int64_t gy_node_stride, int32_t num_nodes, int32_t C, int32_t P,
+                          const float* wt, float* gx, int64_t gx_node_stride, float* ga, int64_t ga_node_stride,
+                          void* stream);
+int64_t mrp_compress_bwd_weight_workspace(int32_t num_nodes, int32_t C, int32_t P, int64_t max_node_stride);
+int mrp_compress_bwd_weight(const float* gy, int64_t gy_node_stride, const float* x, int64_t x_node_stride,
+                            const float* a, int64_t a_node_stride, int32_t num_nodes, int32_t C, int32_t P,
+                            float* gw, float* gbias, void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
  * First layer of the edge encoder, dgl/model/models.py:147-148:  h = relu(pose W1^T + b1).
@@ -317,9 +301,10 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * backward, 1 or 2), "bwd_pre2", "fwd_regular_split" (0, default: whole planes). */
 int mrp_tuning_set(const char* name, int32_t value);
 
-/* Library identification: ABI version (incremented on signature changes; 11 = this header: the
- * epilogue entry points of v10 plus mrp_compress_film_fwd, mrp_compress_dual_fwd,
- * mrp_compress_weight_pack, mrp_film_gate). */
+/* Library identification: ABI version (incremented on signature changes; 12 = this header: the
+ * aggregation and epilogue entry points of v10 plus the matrix-core compress forward and gradients,
+ * mrp_compress_fwd / _bwd_data / _bwd_weight (v11's forward-only fused and two-source compress
+ * kernels, their weight packing and mrp_film_gate are gone)). */
 int mrp_abi_version(void);
 
 /* Human-readable text for a return code (static storage). */

@@ -15,8 +15,7 @@ import threading
 import torch  # noqa: F401  (must be loaded before the HIP library, see module docstring)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-# MRP_GNN_LIB: kernel-lab A/B of an alternative in-tree build (tools/); the product loads lib/libmrp_gnn.so
-LIB_PATH = os.environ.get("MRP_GNN_LIB") or os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
 
 #: Every symbol ``include/mrp_gnn.h`` declares.
 EXPORTED_SYMBOLS = (
@@ -26,10 +25,11 @@ EXPORTED_SYMBOLS = (
     "mrp_film_mean_fwd_ex",
     "mrp_film_mean_bwd_ex",
     "mrp_film_mean_bwd_workspace",
-    "mrp_compress_film_fwd",
-    "mrp_film_gate",
-    "mrp_compress_weight_pack",
-    "mrp_compress_dual_fwd",
+    "mrp_compress_fwd",
+    "mrp_compress_weight_transpose",
+    "mrp_compress_bwd_data",
+    "mrp_compress_bwd_weight_workspace",
+    "mrp_compress_bwd_weight",
     "mrp_edge_hidden_fwd",
     "mrp_edge_encoder_bwd_workspace",
     "mrp_edge_encoder_bwd",
@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 11
+ABI_VERSION = 12
 MAX_NODES = 16
 
 HIP_ERROR_NOT_SUPPORTED = 801  # hipErrorNotSupported: a fused path declines this shape
@@ -93,15 +93,16 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_film_mean_bwd_workspace.restype = ctypes.c_int64
     lib.mrp_tuning_set.argtypes = [ctypes.c_char_p, _I32]
     lib.mrp_tuning_set.restype = ctypes.c_int
-    lib.mrp_compress_film_fwd.argtypes = [_P, _I64, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P,
-                                          _I64, _P]
-    lib.mrp_compress_film_fwd.restype = ctypes.c_int
-    lib.mrp_film_gate.argtypes = [_P, _P, _I64, _P]
-    lib.mrp_film_gate.restype = ctypes.c_int
-    lib.mrp_compress_weight_pack.argtypes = [_P, _P, _I32, _P]
-    lib.mrp_compress_weight_pack.restype = ctypes.c_int
-    lib.mrp_compress_dual_fwd.argtypes = [_P, _I64, _P, _I64, _I32, _I32, _I32, _P, _P, _P, _I64, _P]
-    lib.mrp_compress_dual_fwd.restype = ctypes.c_int
+    lib.mrp_compress_fwd.argtypes = [_P, _I64, _P, _I64, _I32, _I32, _I32, _P, _P, _P, _I64, _P]
+    lib.mrp_compress_fwd.restype = ctypes.c_int
+    lib.mrp_compress_weight_transpose.argtypes = [_P, _P, _I32, _P]
+    lib.mrp_compress_weight_transpose.restype = ctypes.c_int
+    lib.mrp_compress_bwd_data.argtypes = [_P, _I64, _I32, _I32, _I32, _P, _P, _I64, _P, _I64, _P]
+    lib.mrp_compress_bwd_data.restype = ctypes.c_int
+    lib.mrp_compress_bwd_weight_workspace.argtypes = [_I32, _I32, _I32, _I64]
+    lib.mrp_compress_bwd_weight_workspace.restype = ctypes.c_int64
+    lib.mrp_compress_bwd_weight.argtypes = [_P, _I64, _P, _I64, _P, _I64, _I32, _I32, _I32, _P, _P, _P, _I64, _P]
+    lib.mrp_compress_bwd_weight.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]

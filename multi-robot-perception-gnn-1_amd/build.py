@@ -12,10 +12,10 @@ REPO = os.path.dirname(PKG_DIR)
 SOURCES = [os.path.join(PKG_DIR, "csrc", f) for f in ("film_mean_fwd.hip", "film_mean_bwd.hip", "film_mean_bwd_1_8.hip",
                                                     "film_mean_bwd_9_12.hip", "film_mean_bwd_13_16.hip",
                                                     "edge_encoder.hip", "frame_graph.hip",
-                                                    "compress_fused.hip")]
+                                                    "compress_gemm.hip")]
 OBJ_DIR = os.path.join(PKG_DIR, "build")
 HEADERS = [os.path.join(REPO, "include", "mrp_gnn.h")] + [os.path.join(PKG_DIR, "csrc", h) for h in (
-    "film_mean_kernels.hpp", "film_mean_bwd_launch.hpp", "fast_math.hpp")]
+    "film_mean_kernels.hpp", "film_mean_bwd_launch.hpp", "fast_math.hpp", "tuning.hpp")]
 OUT = os.path.join(PKG_DIR, "lib", "libmrp_gnn.so")
 ARCH = os.environ.get("MRP_OFFLOAD_ARCH", "gfx950")
 
@@ -46,10 +46,10 @@ def needs_build(out: str = OUT) -> bool:
 
 
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mcode-object-version=5", "-ffp-contract=off", "-Wno-pass-failed"]
-# per-source extras: the fused compress kernel's producer VALU runs beside MFMAs, where packed f32 ops
-# (SLP-vectorised scalar adds/muls) cost more than the scalar ones (MI355X_MICROARCH.md, filler
-# prices) and would keep the DPP broadcasts from folding into the multiply/add
-EXTRA_FLAGS = {"compress_fused.hip": ["-fno-slp-vectorize"]}
+# per-source extras: the compress GEMMs' only VALU beside the MFMAs is the bias-row sum of the
+# weight gradient, where packed f32 ops (SLP-vectorised scalar adds) cost more than scalar ones
+# (MI355X_MICROARCH.md, filler prices)
+EXTRA_FLAGS = {"compress_gemm.hip": ["-fno-slp-vectorize"]}
 
 
 def _compile(src: str, verbose: bool) -> str:

@@ -1,253 +1,294 @@
-"""The 1x1 compress convolution after the concatenation (``dgl/model/models.py:165-171,183,189``:
-``conv1``/``conv2 = nn.Conv2d(2C, C, kernel_size=1)``) as library GEMMs on the fp32 MFMA.
+"""The 1x1 compress convolution after the concatenation (``dgl/model/models.py:163-165,181-184,186-189``:
+``h = conv(torch.cat((h, g_h), 1))`` with ``conv = nn.Conv2d(2C, C, kernel_size=1)``) and both of its
+gradients on the hand-written fp32 matrix-core kernels of ``csrc/compress_gemm.hip``
+(``include/mrp_gnn.h``: ``mrp_compress_fwd``, ``mrp_compress_bwd_data``, ``mrp_compress_bwd_weight``).
 
-A 1x1 convolution over NCHW is, per node n, ``Y_n = W X_n + b`` with W (C, 2C) shared and X_n the
-node's (2C, H*W) block — a strided-batched GEMM with a broadcast A operand.  Measured on MI355X
-(``tools/exp_compress*.py``): at Nt=256, C=512, 32x32 the batched GEMM takes 2159 us forward and
-2012 us for the input gradient against 2674 / 2363 us for MIOpen's convolution (127 vs 106 TF/s of
-the 157 TF/s fp32 MFMA peak).  The weight gradient ``dW = sum_n dy_n h_n^T`` (``weight_grad_1x1``,
-``tools/exp_compress_wgrad.py``, against MIOpen's weight-gradient convolution with its NCHW -> NHWC
-transposes): on planes of >= 1024 pixels a batched GEMM into an (Nt, C, 2C) temporary + a sum over
-nodes (configs[1] 1.04 vs 1.28 ms, headline size 2.06 vs 2.60 ms); on smaller planes, where K = H W
-is too short for that, channel-major copies of dy and h and ONE GEMM with K = Nt H W (configs[2]
-0.96 vs 1.06 ms, [3] 0.51 vs 0.54, [4] 1.07 vs 1.12).
-Same fp32 arithmetic as the convolution, different summation order: ≤ 1e-5 relative.
+Per node n a 1x1 convolution over NCHW is ``y[n] = W [x[n]; a[n]] + b`` with W (C, 2C) shared, so:
+
+* forward:      one GEMM whose K rows come from two tensors (x and the aggregate) — the (N, 2C, H, W)
+  concatenation is never written;
+* data grad:    ``[dx[n]; da[n]] = W^T dy[n]``, written straight into x's gradient half and the
+  aggregate's gradient (which the aggregation backward then consumes) — no (N, 2C, H, W) buffer;
+* weight grad:  ``dW = sum_n dy[n] [x[n]; a[n]]^T`` and ``db = sum dy`` in one split-K kernel with a
+  fixed-order sum of its partial tiles (deterministic), no (N, C, 2C) temporary, no layout copies.
+
 The module keeps the reference's ``nn.Conv2d`` parameters (``conv1.weight`` (C, 2C, 1, 1),
-``conv1.bias``), so ``state_dict`` keys are unchanged.
+``conv1.bias``), so ``state_dict`` keys are unchanged.  Same fp32 arithmetic as the convolution
+(exact fp32 products), different summation order: checked against float64 (``tests/stack_ref``).
+
+Shapes the kernels decline (C % 32 != 0, H W % 4 != 0 — and, for the weight gradient only,
+H W % 32 != 0 — none of them a reference configuration: the reference's planes are
+``image_size/32`` squares, 8 x 8 at its default) run torch's own GEMMs
+(:func:`set_compress_path` ``"library"`` forces that path everywhere, for A/B measurements).
 """
 from __future__ import annotations
-
-import ctypes
 
 import torch
 
 from . import _lib
 
-
-# the batched-GEMM weight gradient: planes of at least this many pixels, temporaries up to this size
-WGRAD_BMM_MIN_PLANE = 1024
-WGRAD_BMM_MAX_TEMP = 1 << 30
+_PATH = ["hip"]
 
 
-def weight_grad_1x1(h: torch.Tensor, wshape, gy: torch.Tensor) -> torch.Tensor:
-    """``torch.nn.grad.conv2d_weight(h, wshape, gy)`` for a 1x1 conv over (N, K, H, W) input h and
-    (N, C, H, W) output gradient gy (both contiguous fp32), by the faster route for the plane size."""
-    n, k, H, W = h.shape
-    c = wshape[0]
-    P = H * W
-    if P >= WGRAD_BMM_MIN_PLANE and n * c * k * 4 <= WGRAD_BMM_MAX_TEMP:
-        return torch.bmm(gy.reshape(n, c, P), h.reshape(n, k, P).transpose(1, 2)).sum(0).view(wshape)
-    a = gy.reshape(n, c, P).permute(1, 0, 2).reshape(c, n * P)
-    bt = h.reshape(n, k, P).permute(1, 0, 2).reshape(k, n * P)
-    return torch.mm(a, bt.t()).view(wshape)
+def set_compress_path(path: str) -> None:
+    """``"hip"`` (default): the matrix-core kernels above; ``"library"``: the cat kernel + torch's
+    library GEMMs (the round-2 path), for A/B measurement."""
+    if path not in ("hip", "library"):
+        raise ValueError("compress path must be 'hip' or 'library'")
+    _PATH[0] = path
 
 
-class Compress1x1Function(torch.autograd.Function):
+def compress_path() -> str:
+    return _PATH[0]
+
+
+def _nstride(t: torch.Tensor):
+    """Node stride of an (N, C, H, W) fp32 tensor laid out as the kernels need (each node's C H W
+    block contiguous, 16-byte aligned, stride % 4 == 0), else None."""
+    from .aggregate import node_stride
+    s = node_stride(t)
+    if s is None or s % 4 != 0 or t.data_ptr() % 16 != 0:
+        return None
+    return s
+
+
+def _node_major(t: torch.Tensor):
+    s = _nstride(t)
+    if s is None:
+        t = t.contiguous()
+        s = t.shape[1] * t.shape[2] * t.shape[3]
+    return t, s
+
+
+def _weight2d(weight: torch.Tensor) -> torch.Tensor:
+    C = weight.shape[0]
+    w = weight.detach().reshape(C, weight.shape[1])
+    if not w.is_contiguous() or w.dtype != torch.float32:
+        w = w.float().contiguous()
+    return w
+
+
+def conv_is_plain_1x1(conv: torch.nn.Conv2d, C: int) -> bool:
+    return (conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1 and conv.dilation == (1, 1)
+            and conv.padding in ((0, 0), "valid") and tuple(conv.weight.shape[:2]) == (C, 2 * C)
+            and conv.weight.dtype == torch.float32)
+
+
+def kernels_supported(C: int, P: int) -> bool:
+    """The forward and data-gradient kernels: C % 32 == 0, P % 4 == 0 (``include/mrp_gnn.h``)."""
+    return C > 0 and P > 0 and C % 32 == 0 and P % 4 == 0
+
+
+def compress_forward(weight: torch.Tensor, bias, x: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
+    """``conv(torch.cat((x, a), 1))`` for a (C, 2C, 1, 1) weight without the concatenation
+    (``mrp_compress_fwd``); x and a are (N, C, H, W), e.g. views of a cat buffer's halves."""
+    from .aggregate import _ptr, _stream
+    n, C, H, W = x.shape
+    x, xs = _node_major(x)
+    a, as_ = _node_major(a)
+    w = _weight2d(weight)
+    b = bias.detach() if bias is not None else None
+    if b is not None and (b.dtype != torch.float32 or not b.is_contiguous()):
+        b = b.float().contiguous()
+    y = torch.empty((n, C, H, W), device=x.device, dtype=torch.float32)
+    with torch.cuda.device(x.device):
+        _lib.check(_lib.load_library().mrp_compress_fwd(_ptr(x), xs, _ptr(a), as_, n, C, H * W, _ptr(w), _ptr(b),
+                                                        _ptr(y), C * H * W, _stream(x.device)), "mrp_compress_fwd")
+    return y
+
+
+def compress_backward_data(weight: torch.Tensor, gy: torch.Tensor, gx: torch.Tensor = None, ga: torch.Tensor = None):
+    """(gx, ga) = (W[:, :C]^T gy, W[:, C:]^T gy) per node (``mrp_compress_bwd_data``), written into
+    the given (N, C, H, W) outputs (e.g. the halves of a cat buffer's gradient) or new tensors."""
+    from .aggregate import _ptr, _stream
+    n, C, H, W = gy.shape
+    lib = _lib.load_library()
+    gy, gs = _node_major(gy)
+    w = _weight2d(weight)
+    wt = torch.empty((2 * C, C), device=gy.device, dtype=torch.float32)
+    gx = torch.empty((n, C, H, W), device=gy.device, dtype=torch.float32) if gx is None else gx
+    ga = torch.empty((n, C, H, W), device=gy.device, dtype=torch.float32) if ga is None else ga
+    gxs, gas = _nstride(gx), _nstride(ga)
+    if gxs is None or gas is None:
+        raise ValueError("compress_backward_data: outputs must be node-major fp32, 16-byte aligned")
+    st = _stream(gy.device)
+    with torch.cuda.device(gy.device):
+        _lib.check(lib.mrp_compress_weight_transpose(_ptr(w), _ptr(wt), C, st), "mrp_compress_weight_transpose")
+        _lib.check(lib.mrp_compress_bwd_data(_ptr(gy), gs, n, C, H * W, _ptr(wt), _ptr(gx), gxs, _ptr(ga), gas, st),
+                   "mrp_compress_bwd_data")
+    return gx, ga
+
+
+def compress_backward_weight(gy: torch.Tensor, x: torch.Tensor, a: torch.Tensor, want_bias: bool = True):
+    """(dW (C, 2C, 1, 1), db (C) or None) = (sum_n gy[n] [x[n]; a[n]]^T, sum gy)
+    (``mrp_compress_bwd_weight``); None when the kernel declines the shape (H W % 32 != 0)."""
+    from .aggregate import _ptr, _stream
+    n, C, H, W = gy.shape
+    lib = _lib.load_library()
+    gy, gs = _node_major(gy)
+    x, xs = _node_major(x)
+    a, as_ = _node_major(a)
+    dw = torch.empty((C, 2 * C, 1, 1), device=gy.device, dtype=torch.float32)
+    db = torch.empty((C,), device=gy.device, dtype=torch.float32) if want_bias else None
+    nbytes = int(lib.mrp_compress_bwd_weight_workspace(n, C, H * W, max(gs, xs, as_)))
+    ws = torch.empty((nbytes + 3) // 4, device=gy.device, dtype=torch.float32) if nbytes > 0 else None
+    with torch.cuda.device(gy.device):
+        code = lib.mrp_compress_bwd_weight(_ptr(gy), gs, _ptr(x), xs, _ptr(a), as_, n, C, H * W, _ptr(dw), _ptr(db),
+                                           _ptr(ws), nbytes, _stream(gy.device))
+    if code == _lib.HIP_ERROR_NOT_SUPPORTED:
+        return None
+    _lib.check(code, "mrp_compress_bwd_weight")
+    return dw, db
+
+
+# ---- torch library GEMMs: the A/B comparison path and the shapes the kernels decline -------------
+
+def _lib_forward(weight, bias, x, a):
+    n, C, H, W = x.shape
+    cat = torch.cat((x, a), 1).reshape(n, 2 * C, H * W)
+    w2 = weight.reshape(C, 2 * C)
+    y = torch.baddbmm(bias.view(1, C, 1), w2.expand(n, C, 2 * C), cat) if bias is not None else \
+        torch.bmm(w2.expand(n, C, 2 * C), cat)
+    return y.view(n, C, H, W)
+
+
+def _lib_backward_data(weight, gy):
+    n, C, H, W = gy.shape
+    d = torch.bmm(weight.reshape(C, 2 * C).t().expand(n, 2 * C, C), gy.reshape(n, C, H * W)).view(n, 2 * C, H, W)
+    return d[:, :C], d[:, C:]
+
+
+def _lib_backward_weight(gy, x, a, want_bias):
+    n, C, H, W = gy.shape
+    cat = torch.cat((x, a), 1)
+    g2 = gy.reshape(n, C, H * W).permute(1, 0, 2).reshape(C, -1)
+    h2 = cat.reshape(n, 2 * C, H * W).permute(1, 0, 2).reshape(2 * C, -1)
+    return torch.mm(g2, h2.t()).view(C, 2 * C, 1, 1), (gy.sum((0, 2, 3)) if want_bias else None)
+
+
+def _use_kernels(C, P) -> bool:
+    return _PATH[0] == "hip" and kernels_supported(C, P)
+
+
+class CompressFunction(torch.autograd.Function):
+    """``conv(torch.cat((x, a), 1))`` with autograd, x and a separate (N, C, H, W) tensors."""
+
+    @staticmethod
+    def forward(ctx, x, a, weight, bias):
+        n, C, H, W = x.shape
+        hip = _use_kernels(C, H * W)
+        y = compress_forward(weight, bias, x, a) if hip else _lib_forward(weight, bias, x, a)
+        ctx.save_for_backward(x, a, weight)
+        ctx.hip, ctx.has_bias = hip, bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, a, weight = ctx.saved_tensors
+        gx = ga = dw = db = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            gx, ga = compress_backward_data(weight, gy) if ctx.hip else _lib_backward_data(weight, gy)
+        if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
+            r = compress_backward_weight(gy, x, a, ctx.has_bias) if ctx.hip else None
+            dw, db = r if r is not None else _lib_backward_weight(gy, x, a, ctx.has_bias)
+        return gx, ga, dw, db
+
+
+class LibraryCompressFunction(torch.autograd.Function):
+    """``conv(h)`` over a (N, 2C, H, W) concatenation buffer on torch's library GEMMs (the round-2
+    path: batched GEMM forward and data gradient, one GEMM with K = N H W for the weight gradient)."""
+
     @staticmethod
     def forward(ctx, h, weight, bias):
         n, k, H, W = h.shape
-        c = weight.shape[0]
+        C = weight.shape[0]
         h = h.contiguous()
-        w2 = weight.reshape(c, k)
-        x = h.view(n, k, H * W)
-        if bias is not None:
-            y = torch.baddbmm(bias.view(1, c, 1), w2.expand(n, c, k), x)
-        else:
-            y = torch.bmm(w2.expand(n, c, k), x)
+        w2 = weight.reshape(C, k)
+        y = torch.baddbmm(bias.view(1, C, 1), w2.expand(n, C, k), h.view(n, k, H * W)) if bias is not None else \
+            torch.bmm(w2.expand(n, C, k), h.view(n, k, H * W))
         ctx.save_for_backward(h, weight)
         ctx.has_bias = bias is not None
-        return y.view(n, c, H, W)
+        return y.view(n, C, H, W)
 
     @staticmethod
     def backward(ctx, gy):
         h, weight = ctx.saved_tensors
         n, k, H, W = h.shape
-        c = weight.shape[0]
+        C = weight.shape[0]
         gy = gy.contiguous()
         dh = dw = db = None
         if ctx.needs_input_grad[0]:
-            dh = torch.bmm(weight.reshape(c, k).t().expand(n, k, c), gy.view(n, c, H * W)).view(n, k, H, W)
+            dh = torch.bmm(weight.reshape(C, k).t().expand(n, k, C), gy.view(n, C, H * W)).view(n, k, H, W)
         if ctx.needs_input_grad[1]:
-            dw = weight_grad_1x1(h, weight.shape, gy)
+            g2 = gy.reshape(n, C, H * W).permute(1, 0, 2).reshape(C, -1)
+            h2 = h.reshape(n, k, H * W).permute(1, 0, 2).reshape(k, -1)
+            dw = torch.mm(g2, h2.t()).view(weight.shape)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = gy.sum((0, 2, 3))
         return dh, dw, db
 
 
 def compress_1x1(conv: torch.nn.Conv2d, h: torch.Tensor) -> torch.Tensor:
-    """``conv(h)`` for the reference's 1x1 compress conv; batched GEMM on the GPU."""
-    if not h.is_cuda or conv.kernel_size != (1, 1) or conv.stride != (1, 1) or conv.groups != 1 \
-            or conv.padding not in ((0, 0), "valid") or conv.dilation != (1, 1) or h.dtype != torch.float32:
+    """``conv(h)`` for the reference's 1x1 compress conv over a (N, 2C, H, W) concatenation h: the
+    matrix-core kernels read its two halves in place (``set_compress_path('library')``: torch's
+    library GEMMs)."""
+    C = h.shape[1] // 2
+    if not h.is_cuda or h.dtype != torch.float32 or h.shape[1] != 2 * C or not conv_is_plain_1x1(conv, C):
         return conv(h)
-    return Compress1x1Function.apply(h, conv.weight, conv.bias)
-
-
-def _weight_packed(conv: torch.nn.Conv2d) -> torch.Tensor:
-    """The conv weight (C, 2C, 1, 1) in the fused kernel's k4-packed stage layout
-    (``mrp_compress_weight_pack``); cached on the module per weight version."""
-    from .aggregate import _ptr, _stream
-    w = conv.weight
-    key = (w.data_ptr(), w._version, w.device)
-    hit = getattr(conv, "_mrp_wp", None)
-    if hit is not None and hit[0] == key:
-        return hit[1]
-    C = w.shape[0]
-    src = w.detach().reshape(C, 2 * C).contiguous()
-    wp = torch.empty(2 * C * C, device=w.device, dtype=torch.float32)
-    with torch.cuda.device(w.device):
-        _lib.check(_lib.load_library().mrp_compress_weight_pack(_ptr(src), _ptr(wp), C, _stream(w.device)),
-                   "mrp_compress_weight_pack")
-    conv._mrp_wp = (key, wp)
-    return wp
-
-
-def fused_compress_supported(conv: torch.nn.Conv2d, x: torch.Tensor, csr) -> bool:
-    """Whether ``mrp_compress_film_fwd`` covers this layer: fp32 CUDA features, a plain 1x1
-    Conv2d(2C, C), complete graphs of 2..8 nodes, H W % 16 == 0, C % 128 == 0."""
-    if x.dim() != 4:
-        return False
-    n, C, H, W = x.shape
-    if (not x.is_cuda or x.dtype != torch.float32 or conv.kernel_size != (1, 1) or conv.groups != 1
-            or conv.stride != (1, 1) or conv.dilation != (1, 1) or conv.padding not in ((0, 0), "valid")
-            or tuple(conv.weight.shape[:2]) != (C, 2 * C) or conv.weight.dtype != torch.float32):
-        return False
-    return csr.graph_kind == _lib.GRAPH_COMPLETE and 2 <= csr.max_nodes <= 8 and (H * W) % 16 == 0 and C % 128 == 0
-
-
-def compress_film_fused(conv: torch.nn.Conv2d, x: torch.Tensor, gb, csr, mode: int):
-    """``conv(torch.cat((x, film_mean(x, gb)), 1))`` (``models.py:181-184``) in ONE kernel
-    (``mrp_compress_film_fwd``): the aggregate is computed inside the 1x1 GEMM's operand producer and
-    the (N, 2C, H, W) concatenation never reaches HBM.  Forward only (no autograd).  Returns None
-    when the kernel does not cover the shape (non-complete graphs, N > 8, P % 16, C % 128): the
-    caller then runs the cat kernel + batched GEMM."""
-    if not fused_compress_supported(conv, x, csr):
-        return None
-    n, C, H, W = x.shape
-    from .aggregate import _ptr, _stream, node_stride
-    xs = node_stride(x)
-    if xs is None:
-        x = x.contiguous()
-        xs = C * H * W
-    lib = _lib.load_library()
-    if gb is not None:
-        gb = gb.reshape(csr.num_edges, C, 2)
-        if not gb.is_contiguous() or gb.dtype != torch.float32:
-            gb = gb.contiguous().float()
-        if mode & _lib.GB_LOGITS:
-            # one elementwise pass to post-sigmoid pairs (the kernels' own sigmoid: same bits as the
-            # logits path) instead of 2 x E x C sigmoids in every workgroup of a channel column
-            gate = torch.empty_like(gb)
-            with torch.cuda.device(x.device):
-                _lib.check(lib.mrp_film_gate(_ptr(gb), _ptr(gate), gb.numel(), _stream(x.device)), "mrp_film_gate")
-            gb, mode = gate, mode & ~_lib.GB_LOGITS
-    wt = _weight_packed(conv)
-    bias = conv.bias.detach() if conv.bias is not None else None
-    if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
-        bias = bias.float().contiguous()
-    y = torch.empty((n, C, H, W), device=x.device, dtype=torch.float32)
-    with torch.cuda.device(x.device):
-        code = lib.mrp_compress_film_fwd(_ptr(x), xs, _ptr(gb), csr.num_graphs, csr.max_nodes, csr.graph_kind,
-                                         csr.num_nodes, csr.num_edges, C, H * W, mode, _ptr(wt), _ptr(bias),
-                                         _ptr(y), C * H * W, _stream(x.device))
-    if code == _lib.HIP_ERROR_NOT_SUPPORTED:
-        return None
-    _lib.check(code, "mrp_compress_film_fwd")
-    return y
-
-
-def dual_compress_supported(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
-    """Whether ``mrp_compress_dual_fwd`` covers this layer (any graph): fp32 CUDA features, a plain
-    1x1 Conv2d(2C, C), C % 128 == 0, H W % 16 == 0."""
-    if x.dim() != 4:
-        return False
-    n, C, H, W = x.shape
-    return (x.is_cuda and x.dtype == torch.float32 and conv.kernel_size == (1, 1) and conv.groups == 1
-            and conv.stride == (1, 1) and conv.dilation == (1, 1) and conv.padding in ((0, 0), "valid")
-            and tuple(conv.weight.shape[:2]) == (C, 2 * C) and conv.weight.dtype == torch.float32
-            and C % 128 == 0 and (H * W) % 16 == 0)
-
-
-def compress_dual(conv: torch.nn.Conv2d, x: torch.Tensor, agg: torch.Tensor):
-    """``conv(torch.cat((x, agg), 1))`` for a 1x1 ``Conv2d(2C, C)`` without the concatenation:
-    ``mrp_compress_dual_fwd`` (fp32 MFMA, operands staged by LDS-DMA).  Forward only.  None when the
-    kernel does not cover the shape (C % 128, H W % 16, alignment)."""
-    n, C, H, W = x.shape
-    if not dual_compress_supported(conv, x) or agg.shape != x.shape or agg.dtype != torch.float32:
-        return None
-    from .aggregate import _ptr, _stream, node_stride
-    xs, gs = node_stride(x), node_stride(agg)
-    if xs is None:
-        x = x.contiguous()
-        xs = C * H * W
-    if gs is None:
-        agg = agg.contiguous()
-        gs = C * H * W
-    wt = _weight_packed(conv)
-    bias = conv.bias.detach() if conv.bias is not None else None
-    if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
-        bias = bias.float().contiguous()
-    y = torch.empty((n, C, H, W), device=x.device, dtype=torch.float32)
-    lib = _lib.load_library()
-    with torch.cuda.device(x.device):
-        code = lib.mrp_compress_dual_fwd(_ptr(x), xs, _ptr(agg), gs, n, C, H * W, _ptr(wt), _ptr(bias), _ptr(y),
-                                         C * H * W, _stream(x.device))
-    if code == _lib.HIP_ERROR_NOT_SUPPORTED:
-        return None
-    _lib.check(code, "mrp_compress_dual_fwd")
-    return y
-
+    if _PATH[0] == "library":
+        return LibraryCompressFunction.apply(h, conv.weight, conv.bias)
+    return CompressFunction.apply(h[:, :C], h[:, C:], conv.weight, conv.bias)
 
 
 class FilmCompressFunction(torch.autograd.Function):
     """``conv(torch.cat((x, film_mean(x, gb)), 1))`` (``models.py:181-184``) with autograd and without
     the concatenation: forward = the aggregation kernel into its own (N, C, H, W) output, then the
-    two-source MFMA compress (``mrp_compress_dual_fwd``) reading x and the aggregate in place.
-    Backward: ``d cat = W^T dy`` (one batched GEMM into an (N, 2C, H, W) buffer, as the cat path's),
-    then ONE aggregation-backward pass with the first half as the base of x's gradient (so x's two
-    gradient terms are never added by a separate kernel), and the weight gradient as two half-width
-    GEMMs (x and the aggregate are separate tensors here).  Saves, per layer, the concatenation's
-    second copy of x (written by the cat kernel, read by the GEMM) and keeps the aggregate instead of
-    the 2C-channel buffer for backward."""
+    two-source compress.  Backward: ``[gx; ga] = W^T dy`` by the data-gradient kernel, ONE
+    aggregation-backward pass with ga as its grad_out and gx as the base of x's gradient (x's two
+    gradient terms are never added by a separate kernel), and the weight gradient from x and the
+    saved aggregate.  Saves x, gb and the aggregate — not a 2C-channel buffer."""
 
     @staticmethod
-    def forward(ctx, x, gb, weight, bias, conv, csr, mode: int):
+    def forward(ctx, x, gb, weight, bias, csr, mode: int):
         from .aggregate import film_mean_forward_into
+        n, C, H, W = x.shape
         agg = torch.empty(x.shape, device=x.device, dtype=torch.float32)
         film_mean_forward_into(x, gb, csr, mode, agg)
-        y = compress_dual(conv, x, agg)
-        if y is None:
-            raise RuntimeError("mrp_compress_dual_fwd does not cover this shape (callers check "
-                               "dual_compress_supported first)")
+        hip = _use_kernels(C, H * W)
+        y = compress_forward(weight, bias, x, agg) if hip else _lib_forward(weight, bias, x, agg)
         ctx.save_for_backward(x, gb, agg, weight)
-        ctx.csr, ctx.mode, ctx.has_bias = csr, mode, bias is not None
+        ctx.csr, ctx.mode, ctx.has_bias, ctx.hip = csr, mode, bias is not None, hip
         return y
 
     @staticmethod
     def backward(ctx, gy):
         from .aggregate import film_mean_backward
         x, gb, agg, weight = ctx.saved_tensors
-        n, C, H, W = x.shape
-        gy = gy.contiguous()
         need_x, need_gb = ctx.needs_input_grad[0], gb is not None and ctx.needs_input_grad[1]
         dx = dgb = dw = db = None
         if need_x or need_gb:
-            dcat = torch.bmm(weight.reshape(C, 2 * C).t().expand(n, 2 * C, C), gy.view(n, C, H * W))
-            dcat = dcat.view(n, 2 * C, H, W)
-            dx, dgb = film_mean_backward(dcat[:, C:], x, gb, ctx.csr, ctx.mode, need_x, need_gb,
-                                         grad_x_base=dcat[:, :C] if need_x else None)
+            gx, ga = compress_backward_data(weight, gy) if ctx.hip else _lib_backward_data(weight, gy)
+            dx, dgb = film_mean_backward(ga, x, gb, ctx.csr, ctx.mode, need_x, need_gb,
+                                         grad_x_base=gx if need_x else None)
             if dgb is not None:
                 dgb = dgb.view(gb.shape).to(gb.dtype)
-        if ctx.needs_input_grad[2]:
-            half = (C, C, 1, 1)
-            dw = torch.cat((weight_grad_1x1(x.contiguous(), half, gy), weight_grad_1x1(agg, half, gy)), 1)
-        if ctx.has_bias and ctx.needs_input_grad[3]:
-            db = gy.sum((0, 2, 3))
-        return dx, dgb, dw, db, None, None, None
+        if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
+            r = compress_backward_weight(gy, x, agg, ctx.has_bias) if ctx.hip else None
+            dw, db = r if r is not None else _lib_backward_weight(gy, x, agg, ctx.has_bias)
+            if not ctx.needs_input_grad[2]:
+                dw = None
+        return dx, dgb, dw, db, None, None
+
+
+def film_compress_supported(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
+    """Whether :func:`film_compress` takes this layer: fp32 CUDA (N, C, H, W) features and a plain 1x1
+    ``Conv2d(2C, C)`` (the matrix-core kernels, or torch's GEMMs for shapes they decline)."""
+    return x.dim() == 4 and x.is_cuda and x.dtype == torch.float32 and conv_is_plain_1x1(conv, x.shape[1])
 
 
 def film_compress(conv: torch.nn.Conv2d, x: torch.Tensor, gb, csr, mode: int) -> torch.Tensor:
     """Autograd form of ``conv(torch.cat((x, film_mean(x, gb)), 1))`` without the concatenation
-    (``FilmCompressFunction``); the caller checks ``dual_compress_supported(conv, x)``."""
+    (:class:`FilmCompressFunction`); the caller checks :func:`film_compress_supported`."""
     if gb is not None:
         gb = gb.reshape(csr.num_edges, x.shape[1], 2)
-    return FilmCompressFunction.apply(x, gb, conv.weight, conv.bias, conv, csr, mode)
+    return FilmCompressFunction.apply(x, gb, conv.weight, conv.bias, csr, mode)

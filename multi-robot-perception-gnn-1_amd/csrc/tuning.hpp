@@ -1,0 +1,41 @@
+// tuning.hpp — launch knobs shared by the kernel files (defaults = the measured optima;
+// mrp_tuning_set changes them for lab sweeps).
+#pragma once
+
+namespace mrp_host {
+
+// Launch geometry knobs (defaults = the measured optima; mrp_tuning_set changes them for lab sweeps).
+struct Tuning {
+  int fwd_lo = 16, fwd_hi = 64, fwd_cap = 16;  // film_fwd: lanes per plane in [lo, hi], <= cap channels
+  int fwd_vec2_below = 0;  // film_fwd: 8-byte slices for planes of fewer than this many pixels (lab knob)
+  // film_fwd_regular: whole planes, 32 lanes each (k-NN(4) N=16 C=1024 16x16, B=8: 54.1 us against
+  // 57.0 us split over 2 workgroups with 32 lanes; tools/sweep_geometry.py)
+  int fwd_regular_split = 0;
+  int fwd_regular_lo = 32, fwd_regular_hi = 32, fwd_regular_cap = 16;
+  // film_bwd_fused (N <= 8): at most 16 channels per workgroup — at 8x8 planes (8 lanes per plane)
+  // two-wave workgroups: configs[3] 24.3 vs 25.6 us with 8 channels, configs[2] 54.7-54.9 vs 55.2
+  // (tools/sweep_geometry.py smallbwd; 32 channels: 67.2 vs 60.8 us at C=1280 in round 1); 32x32
+  // planes are unaffected (2 channels of 128 lanes)
+  int bwd_fused_lo = 8, bwd_fused_hi = 128, bwd_fused_cap = 16;
+  int bwd_pre2 = 1;  // film_bwd_fused: prefetch both slices when a lane owns exactly two
+  int bwd_regular_vec = 2, bwd_regular_lanes = 16;              // film_bwd_regular (N > 8, k-NN)
+  // film_bwd_mfma (Gram and grad_x on the matrix cores; P % 64 == 0, 16-byte aligned operands):
+  // regular graphs of 9..16 nodes (0 = film_bwd_regular), complete graphs (1; default 0: film_bwd_fused
+  // measured faster at every config: 143 vs 159 us at configs[1], 59 vs 64 at [2], 27 vs 29 at [3])
+  int bwd_regular_mfma = 1;
+  int bwd_complete_mfma = 0;
+  int bwd_mfma_cpw = 2;  // film_bwd_mfma: 16-row blocks per wave (1 or 2)
+  // film_bwd_regular: split planes so each lane owns this many slices (0: whole planes); needs the
+  // caller's workspace (mrp_film_mean_bwd_workspace), else whole planes.  Measured slower at the
+  // configs[4] shape (k-NN(4) N=16 C=1024 16x16 B=8: 102.7 us whole planes, 113 / 131 / 170 us at
+  // 4 / 2 / 1 slices per lane): each extra workgroup repeats a prologue of dependent loads that the
+  // 2-waves-per-SIMD kernel cannot hide.  Off by default; kept as a tested experiment path.
+  int bwd_regular_slices = 0;
+
+  // compress GEMMs (compress_gemm.hip): kernel variant of the forward / data-gradient product (NN) and
+  // of the weight-gradient product (NT); see the variant table there
+  int gemm_nn = -1, gemm_nt = -1;  // -1: the per-shape default
+};
+Tuning& tuning();
+
+}  // namespace mrp_host

@@ -8,7 +8,7 @@ Mirrors ``dgl/model/models.py``:
   and ``forward(g, feats)`` (the north-star signature).  Aggregation runs in the HIP kernel.
 * :class:`GCNBlock`      — the GCN stacking of ``multi_view_dgl_model.forward`` (``models.py:180-189``):
   ``gcn1 -> cat -> [conv1] -> [gcn2 -> cat -> conv2]``, keys ``gcn1.*``, ``conv1.*``, ``gcn2.*``, ``conv2.*``;
-  the 1x1 convs run as batched GEMMs (``compress.py``).
+  the 1x1 convs run on the matrix-core compress kernels without the concatenation (``compress.py``).
 * :class:`GCNStack`      — the same for k layers (``opt.gcn_layers``; BASELINE configs[4] runs 3) and
   the residual (``dgl_models.py:36-37``) / initial-feature-mix combinations, each fused into the
   aggregation kernel's epilogue.
@@ -34,8 +34,7 @@ import torch
 import torch.nn as nn
 
 from .aggregate import film_mean, film_mean_cat, film_mean_mix, film_mean_residual
-from .compress import (compress_1x1, compress_dual, compress_film_fused, dual_compress_supported, film_compress,
-                       fused_compress_supported)
+from .compress import compress_1x1, compress_path, film_compress, film_compress_supported
 from .encoder import edge_logits
 
 
@@ -131,33 +130,15 @@ class GCN(nn.Module):
 
 
     def forward_cat_compress(self, g, feats: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
-        """``conv(torch.cat((feats, self(g, feats)), 1))`` (``models.py:181-184``).  Without autograd
-        (eval, ``test_dgl``), on the planes where it measured faster (``set_fused_compress``), the
-        concatenation is never written: the aggregate kernel, then the two-source MFMA compress
-        (``mrp_compress_dual_fwd``), or the single fused kernel (``mrp_compress_film_fwd``) in
-        "fused" mode; otherwise (and with autograd) the cat kernel + batched GEMM, or, opted in with
-        ``set_training_compress(True)``, the two-source forward with its own backward
-        (``FilmCompressFunction``)."""
+        """``conv(torch.cat((feats, self(g, feats)), 1))`` (``models.py:181-184``) without the
+        concatenation: the aggregation kernel into its own buffer, then the matrix-core compress
+        reading x and the aggregate in place, and in backward the data-gradient kernel writing x's
+        gradient half and the aggregate's gradient straight into the aggregation backward, plus the
+        split-K weight-gradient kernel (``compress.FilmCompressFunction``).  With
+        ``compress.set_compress_path('library')``: the cat kernel + torch's library GEMMs."""
         x = feats
-        setting = fused_compress_setting()
-        if (x.is_cuda and self._return_mode() != "input" and not torch.is_grad_enabled()
-                and fused_compress_enabled(x.shape[-2] * x.shape[-1])):
-            if setting == "fused":
-                if (_opt(self.opt, "gcn_mode", "film_mean") != "copy_mean"
-                        and fused_compress_supported(conv, x, g.csr(x.device))):
-                    mode = _lib_modes()[_opt(self.opt, "gcn_mode", "film_mean")]
-                    z = self.edge_encoder.logits(g.edata["pose"])
-                    y = compress_film_fused(conv, x, z, g.csr(x.device), mode | _lib_logits())
-                    if y is not None:
-                        return y
-            elif dual_compress_supported(conv, x):
-                y = compress_dual(conv, x, self(g, x))
-                if y is not None:
-                    return y
-        if (_TRAIN_DUAL[0] and x.is_cuda and torch.is_grad_enabled() and self._return_mode() != "input"
-                and dual_compress_supported(conv, x)):
-            # opt-in training path: the concatenation-free forward with its own backward
-            # (FilmCompressFunction; set_training_compress)
+        if (x.is_cuda and self._return_mode() != "input" and compress_path() == "hip"
+                and film_compress_supported(conv, x)):
             mode = _opt(self.opt, "gcn_mode", "film_mean")
             if mode == "copy_mean":
                 return film_compress(conv, x, None, g.csr(x.device), _lib_modes()[mode])
@@ -188,46 +169,6 @@ class GCN(nn.Module):
             return film_mean_mix(x, None, g.csr(x.device), x0, alpha, mode)
         z = self.edge_encoder.logits(g.edata["pose"])
         return film_mean_mix(x, z, g.csr(x.device), x0, alpha, mode, logits=True)
-
-
-_FUSED_COMPRESS = ["auto"]
-# "auto": the concatenation-free compress where it measured faster than cat kernel + library GEMM
-# (DESIGN.md §3.6): planes of >= 1024 pixels (configs[1], 32x32: aggregate 92 us + two-source GEMM
-# 1.05 ms = 1.14 ms vs 1.24 ms per layer); at 16x16 (configs[4]: 1.09 vs 1.07 ms) and 8x8
-# (configs[2] 0.85 vs 0.81 ms, [3] 0.54 vs 0.51 ms) the cat kernel + library GEMM stays
-# (tools/exp_compress_dual.py, both paths timed alternately on the same box)
-FUSED_MIN_PLANE = 1024
-
-
-# Training through FilmCompressFunction (no concatenation; backward: W^T dy, one aggregation-backward
-# pass, two half-width weight-gradient GEMMs).  Off: at configs[1] the step measured 8.18 ms either
-# way (tools/exp_train_dual.py) — the forward's saving is spent on the two half-width MIOpen weight
-# gradients and their layout transposes (2.36 + 0.78 ms against 2.13 + 0.62 ms for one full call).
-_TRAIN_DUAL = [False]
-
-
-def set_training_compress(enabled: bool) -> None:
-    """Opt the autograd (training) GCN layer into the concatenation-free compress (True) or keep
-    the cat kernel + batched GEMM (False, default)."""
-    _TRAIN_DUAL[0] = bool(enabled)
-
-
-def fused_compress_enabled(plane: int = None) -> bool:
-    v = _FUSED_COMPRESS[0]
-    if v == "auto":
-        return plane is not None and plane >= FUSED_MIN_PLANE
-    return bool(v)
-
-
-def fused_compress_setting():
-    return _FUSED_COMPRESS[0]
-
-
-def set_fused_compress(enabled) -> None:
-    """The concatenation-free compress of the inference path: True (aggregate kernel + two-source
-    MFMA GEMM wherever it covers the shape), "fused" (the single fused kernel instead), False (cat
-    kernel + library GEMM) or "auto" (default: the two-source path where it measured faster)."""
-    _FUSED_COMPRESS[0] = enabled if enabled in ("auto", "fused") else bool(enabled)
 
 
 def _lib_modes():
