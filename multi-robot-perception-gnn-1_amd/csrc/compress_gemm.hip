@@ -74,9 +74,9 @@ struct Cfg {
 using V0 = Cfg<16, 32, 2, 2, 2>;  // 128 x 128, 64 KiB: two workgroups per CU
 using V1 = Cfg<32, 32, 2, 2, 2>;  // the same on 32x32x2 MFMAs
 using V2 = Cfg<16, 32, 2, 4, 2>;  // 256 x 128, 96 KiB
-using V3 = Cfg<16, 32, 3, 2, 2>;  // three buffers, two stages in flight, 96 KiB
-using V4 = Cfg<16, 64, 2, 2, 2>;  // 64-deep stages, 128 KiB
-using V5 = Cfg<16, 32, 2, 2, 4>;  // 128 x 256, 96 KiB
+using V3 = Cfg<32, 32, 2, 4, 2>;  // the same on 32x32x2 MFMAs
+using V4 = Cfg<32, 64, 2, 2, 2>;  // 64-deep stages, 128 KiB
+using V5 = Cfg<32, 32, 2, 2, 4>;  // 128 x 256, 96 KiB
 #define MRP_CG_VARIANTS(X) X(0, V0) X(1, V1) X(2, V2) X(3, V3) X(4, V4) X(5, V5)
 constexpr int kVariants = 6;
 
@@ -105,21 +105,45 @@ __device__ __forceinline__ int swz_a(int row) {
   return BK == 32 ? (row >> 1) & 7 : row & 15;
 }
 
-// Wait until this wave's pieces of the oldest stage in flight have landed (N = pieces of the younger
-// stages allowed to remain), then the workgroup barrier.  With more than one stage in flight the
-// barrier is the raw s_barrier: __syncthreads() would wait vmcnt(0) and drain the younger stages.
-template <class G>
-__device__ __forceinline__ void stage_sync(bool last) {
-  if constexpr (G::NBUF == 2) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  } else {
-    if (last)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((G::NBUF - 2) * (G::PA + G::PB)) : "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+// The K loop, two LDS buffers, software-pipelined across the barrier.  Per stage s (buffer s & 1) the
+// fragments of group g + 1 are read before the MFMAs of group g; before the last group's MFMAs the
+// wave retires its LDS-DMA pieces of stage s + 1 (vmcnt: the barrier's fence does not count DMA
+// writes) and passes the barrier that (a) publishes stage s + 1 to every wave and (b) certifies that
+// every wave holds its stage-s fragments in registers, so stage s + 2 may be DMA'd into buffer s & 1;
+// then stage s + 1's first fragments are read under stage s's last MFMA group.  One barrier per
+// stage and no LDS latency exposed after it.  The loop is unrolled by 2 so every LDS offset is an
+// immediate.  issue(stage, buf), read(buf, g, frags), mma(frags).
+template <class G, class Issue, class Read, class Mma>
+__device__ __forceinline__ void kloop(int nst, Issue&& issue, Read&& read, Mma&& mma) {
+  static_assert(G::NBUF == 2, "kloop: two LDS buffers");
+  constexpr int NG = G::BK / 16;
+  typedef float Frag[2][G::FB][G::T];  // [A | B][block][k-step]
+  Frag f[2];
+  if (nst <= 0) return;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (nst > 1) issue(1, 1);
+  read(0, 0, f[0]);
+  for (int s0 = 0; s0 < nst; s0 += 2) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int s = s0 + b;
+      if (s < nst) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          if (g + 1 < NG) {
+            read(b, g + 1, f[(g + 1) & 1]);
+          } else if (s + 1 < nst) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (s + 2 < nst) issue(s + 2, b);
+            read(1 - b, 0, f[(g + 1) & 1]);
+          }
+          mma(f[g & 1]);
+        }
+      }
+    }
   }
 }
 
@@ -293,36 +317,16 @@ __global__ void __launch_bounds__(G::THREADS, G::WG_PER_CU) gemm_nn(NNArgs a) {
       for (int r = 0; r < AC::R; ++r) acc[mb][nb][r] = 0.f;
 
   const float* smem = reinterpret_cast<const float*>(smem4);
-  auto compute = [&](const float* As) {
+  auto read = [&](int buf, int g, float (&fr)[2][G::FB][G::T]) {
+    const float* As = smem + buf * G::BUF;
     const float* Bs = As + G::A_FLOATS;
 #pragma unroll
-    for (int g = 0; g < G::BK / 16; ++g) {
-      float af[G::FB][G::T], bf[G::FB][G::T];
+    for (int mb = 0; mb < G::FB; ++mb) read_a<G>(As, aoff, g, mb, fr[0][mb]);
 #pragma unroll
-      for (int mb = 0; mb < G::FB; ++mb) read_a<G>(As, aoff, g, mb, af[mb]);
-#pragma unroll
-      for (int nb = 0; nb < G::FB; ++nb) read_bnn<G>(Bs, boff, g, nb, bf[nb]);
-      mma_group<G>(acc, af, bf);
-    }
+    for (int nb = 0; nb < G::FB; ++nb) read_bnn<G>(Bs, boff, g, nb, fr[1][nb]);
   };
-  const int nst = a.K / G::BK;
-#pragma unroll
-  for (int p = 0; p < G::NBUF - 1; ++p)
-    if (p < nst) issue(p, p);
-  // the loop is unrolled by NBUF so every buffer's LDS offsets are compile-time immediates
-  for (int s0 = 0; s0 < nst; s0 += G::NBUF) {
-#pragma unroll
-    for (int b = 0; b < G::NBUF; ++b) {
-      const int s = s0 + b;
-      if (s < nst) {
-        // LDS-DMA writes count on the issuing wave's vmcnt only; the barrier then publishes the stage
-        // to every wave and certifies that the buffer refilled next is no longer read
-        stage_sync<G>(s + 1 >= nst);
-        if (s + G::NBUF - 1 < nst) issue(s + G::NBUF - 1, (b + G::NBUF - 1) % G::NBUF);
-        compute(smem + b * G::BUF);
-      }
-    }
-  }
+  auto mma = [&](const float (&fr)[2][G::FB][G::T]) { mma_group<G>(acc, fr[0], fr[1]); };
+  kloop<G>(a.K / G::BK, issue, read, mma);
 
   // ---- epilogue: accumulator (row, col) of each block, + bias, to the row's destination
 #pragma unroll
@@ -405,7 +409,7 @@ __global__ void __launch_bounds__(G::THREADS, G::WG_PER_CU) gemm_nt(NTArgs a) {
   }
   // stage position (node relative to node0, pixel) of the next stage to issue: scalar bookkeeping
   int st_node = 0, st_p = (int)(kbeg - node0 * a.P);
-  auto issue = [&](int buf) {
+  auto issue = [&](int, int buf) {  // stages are issued in order: the position advances per call
     const uint32_t sa = (uint32_t)(((int64_t)st_node * a.gs + st_p) * 4);
     const uint32_t sx = (uint32_t)(((int64_t)st_node * a.s0s + st_p) * 4);
     const uint32_t sg = (uint32_t)(((int64_t)st_node * a.s1s + st_p) * 4);
@@ -443,42 +447,27 @@ __global__ void __launch_bounds__(G::THREADS, G::WG_PER_CU) gemm_nt(NTArgs a) {
   }
 
   const float* smem = reinterpret_cast<const float*>(smem4);
-  auto compute = [&](const float* As) {
+  auto read = [&](int buf, int g, float (&fr)[2][G::FB][G::T]) {
+    const float* As = smem + buf * G::BUF;
     const float* Bs = As + G::A_FLOATS;
 #pragma unroll
-    for (int g = 0; g < G::BK / 16; ++g) {
-      float af[G::FB][G::T], bf[G::FB][G::T];
+    for (int mb = 0; mb < G::FB; ++mb) read_a<G>(As, aoff, g, mb, fr[0][mb]);
 #pragma unroll
-      for (int mb = 0; mb < G::FB; ++mb) read_a<G>(As, aoff, g, mb, af[mb]);
-#pragma unroll
-      for (int nb = 0; nb < G::FB; ++nb) read_a<G>(Bs, boff, g, nb, bf[nb]);
-      if (do_db) {
-#pragma unroll
-        for (int mb = 0; mb < G::FB; ++mb) {
-          float s4 = 0.f;
-#pragma unroll
-          for (int t = 0; t < G::T; ++t) s4 += af[mb][t];
-          dbs[mb] += s4;
-        }
-      }
-      mma_group<G>(acc, af, bf);
-    }
+    for (int nb = 0; nb < G::FB; ++nb) read_a<G>(Bs, boff, g, nb, fr[1][nb]);
   };
-  const int nst = kend > kbeg ? (int)((kend - kbeg) / G::BK) : 0;
+  auto mma = [&](const float (&fr)[2][G::FB][G::T]) {
+    if (do_db) {
 #pragma unroll
-  for (int p = 0; p < G::NBUF - 1; ++p)
-    if (p < nst) issue(p);
-  for (int s0 = 0; s0 < nst; s0 += G::NBUF) {
+      for (int mb = 0; mb < G::FB; ++mb) {
+        float s4 = 0.f;
 #pragma unroll
-    for (int b = 0; b < G::NBUF; ++b) {
-      const int s = s0 + b;
-      if (s < nst) {
-        stage_sync<G>(s + 1 >= nst);
-        if (s + G::NBUF - 1 < nst) issue((b + G::NBUF - 1) % G::NBUF);
-        compute(smem + b * G::BUF);
+        for (int t = 0; t < G::T; ++t) s4 += fr[0][mb][t];
+        dbs[mb] += s4;
       }
     }
-  }
+    mma_group<G>(acc, fr[0], fr[1]);
+  };
+  kloop<G>(kend > kbeg ? (int)((kend - kbeg) / G::BK) : 0, issue, read, mma);
 
   float* out = a.out + (int64_t)split * a.M * a.N;
 #pragma unroll

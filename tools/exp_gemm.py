@@ -49,13 +49,13 @@ for name in args.shapes:
     with torch.no_grad():
         ref_y = torch.baddbmm(b.view(1, C, 1), w2.expand(n, C, 2 * C), cat.view(n, 2 * C, P)).view(n, C, H, H)
         ref_d = torch.bmm(w2.t().expand(n, 2 * C, C), gy.view(n, C, P)).view(n, 2 * C, H, H)
-        ref_w = cp.weight_grad_1x1(cat, w.shape, gy)
+        ref_w = cp._lib_backward_weight(gy, x, a, False)[0]
         if args.library:
             it = args.iters
             t_fl = time_launches([lambda: torch.baddbmm(b.view(1, C, 1), w2.expand(n, C, 2 * C), cat.view(n, 2 * C, P))],
                                  it, dev)
             t_dl = time_launches([lambda: torch.bmm(w2.t().expand(n, 2 * C, C), gy.view(n, C, P))], it, dev)
-            t_wl = time_launches([lambda: (cp.weight_grad_1x1(cat, w.shape, gy), gy.sum((0, 2, 3)))], it, dev)
+            t_wl = time_launches([lambda: cp._lib_backward_weight(gy, x, a, True)], it, dev)
             print(f"{name} Nt={n} C={C} {H}x{H} library: fwd {t_fl * 1e6:7.1f} us {tf(t_fl):5.1f} | data {t_dl * 1e6:7.1f} "
                   f"{tf(t_dl):5.1f} | weight {t_wl * 1e6:7.1f} {tf(t_wl):5.1f}", flush=True)
         for v in [int(s) for s in args.variants.split(",")]:
