@@ -24,8 +24,11 @@ Extra JSON fields:
   Cache.  configs[3] and [4] are data-parallel configs: with N > 1 ranks their global batch (32 and
   64 graphs) is split over the ranks (``dist.shard_graph``, "strong"), and the training step
   all-reduces the gradients over RCCL; with one rank they run the per-GPU share (8 graphs).
+* ``configs[0]`` — the reference's CPU-runnable case (4-robot graphs, 64 x 32 x 32, 1 layer, batch 8):
+  the CPU oracle's rate beside the HIP layer's at the same shape (rank 0, N = 1).
 * ``cpu_baseline`` — the CPU oracle (a torch restatement of the reference DGL UDF path, same op
-  sequence) on the headline workload, rank 0 at N=1 only, bounded in time.
+  sequence) on the headline workload, rank 0 at N=1 only, bounded in time; threads = the job's CPU
+  share (OMP_NUM_THREADS) or the affinity mask, with the host's counts reported beside it.
 """
 from __future__ import annotations
 
@@ -152,11 +155,49 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def cpu_threads():
+    """Threads for the CPU baseline: the job's CPU share (OMP_NUM_THREADS, which the GPU pool sets to
+    the per-GPU share of the host) or else every CPU this process may run on; plus what the host has."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = int(omp) if omp and omp.isdigit() and int(omp) > 0 else aff
+    return threads, {"os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": omp,
+                     "threads_used": threads}
+
+
+def cpu_oracle_rate(B, N, C, H, W, seconds, knn=None):
+    """elems/s of the oracle GCN forward (the reference op sequence on the host) over about
+    ``seconds`` of CPU work, with the baseline's thread count."""
+    import oracle
+    threads, _ = cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        g = make_workload(B, N, C, H, W, seed=1234, device="cpu", knn=knn)
+        torch.manual_seed(0)
+        enc = mrp.edge_encoder([C, C])
+        params = dict(enc.named_parameters())
+        src, dst = (t.numpy() for t in g.edges())
+        x, pose = g.ndata["image"], g.edata["pose"]
+        with torch.no_grad():
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                oracle.gcn_forward(params, x, pose, src, dst)
+                reps += 1
+                el = time.perf_counter() - t0
+                if el >= seconds:
+                    break
+    finally:
+        torch.set_num_threads(prev)
+    return x.numel() * reps / el, reps, el, threads
+
+
 def cpu_baseline(B, N, C, H, W, seconds):
     """The reference op sequence on the host (oracle: edge encoder -> gather -> FiLM -> degree
     bucket -> mean) over the headline workload itself, bounded to about ``seconds`` of CPU work."""
     import oracle
-    threads = torch.get_num_threads()
+    threads, counts = cpu_threads()
+    torch.set_num_threads(threads)
     g = make_workload(B, N, C, H, W, seed=1234, device="cpu")
     torch.manual_seed(0)
     enc = mrp.edge_encoder([C, C])
@@ -174,9 +215,49 @@ def cpu_baseline(B, N, C, H, W, seconds):
             if el >= seconds:
                 break
     return {"value": elems * reps / el, "unit": "elems/s", "cores": threads, "kind": "port",
-            "cpu": cpu_model(),
+            "cpu": cpu_model(), "host": counts,
+            "threads_note": "the job's CPU share (OMP_NUM_THREADS, set by the GPU pool to the per-GPU share "
+                            "of the host) when set, else every CPU in the process's affinity mask",
             "sample": f"the headline workload itself ({B} graphs x N={N} x C={C} x {H}x{W}), {reps} forward "
                       f"passes in {el:.1f} s, torch CPU fp32, {threads} threads"}
+
+
+def config0_record(device, args):
+    """BASELINE configs[0]: the reference's CPU-runnable case — 4-robot complete graphs, 64 x 32 x 32
+    node features, one GCN layer, batch 8 (dgl/training.py:28 default), on the DGL CPU path
+    (dgl/training.py:176-218 plumbing).  DGL is absent, so the CPU number is the oracle (the same op
+    sequence in torch); beside it the HIP layer on the GPU at the same shape."""
+    B, N, C, H = 8, 4, 64, 32
+    g = make_workload(B, N, C, H, H, seed=77, device=device)
+    torch.manual_seed(0)
+    gcn = mrp.GCN(types.SimpleNamespace(feature_dim=C)).to(device)
+    x = g.ndata["image"]
+    with torch.no_grad():
+        for _ in range(10):
+            gcn(g, x)
+        t = timed(lambda: gcn(g, x), 50, 1, device, args.dist_backend)
+    xr = x.detach().clone().requires_grad_(True)
+    gy = torch.randn_like(x)
+
+    def train():
+        for p in gcn.parameters():
+            p.grad = None
+        gcn(g, xr).backward(gy)
+
+    for _ in range(5):
+        train()
+    tt = timed(train, 20, 1, device, args.dist_backend)
+    rec = {"config": "configs[0]: 4-robot complete graph, random 64x32x32 node feats, 1 GraphConv layer, "
+                     "DGL CPU backend (dgl/training.py plumbing)",
+           "graphs": B, "robots": N, "channels": C, "H": H, "W": H, "layers": 1,
+           "gpu_forward": {"value": x.numel() / t, "unit": "elems/s", "ms_per_step": t * 1e3},
+           "gpu_train_step": {"value": x.numel() / tt, "unit": "elems/s", "ms_per_step": tt * 1e3}}
+    if not args.no_cpu_baseline:
+        rate, reps, el, threads = cpu_oracle_rate(B, N, C, H, H, min(args.cpu_seconds, 5.0))
+        rec["cpu_forward"] = {"value": rate, "unit": "elems/s", "kind": "port", "cores": threads,
+                              "sample": f"{reps} oracle forward passes in {el:.1f} s, torch CPU fp32"}
+        rec["gpu_over_cpu"] = rec["gpu_forward"]["value"] / rate
+    return rec
 
 
 def graph_build_time(B, N, device, reps=20):
@@ -402,7 +483,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step measurement")
     ap.add_argument("--train-steps", type=int, default=20)
-    ap.add_argument("--configs", default="1,2,3,4", help="BASELINE configs to measure ('' for none)")
+    ap.add_argument("--configs", default="0,1,2,3,4", help="BASELINE configs to measure ('' for none)")
     ap.add_argument("--config-steps", type=int, default=10)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (control-flow tests)")
     args = ap.parse_args()
@@ -457,7 +538,11 @@ def main():
     train = None if args.no_train else train_step_time(gcn, g, x, world, device, args)
     configs = {}
     for cid in [int(c) for c in args.configs.split(",") if c.strip()]:
-        configs[f"configs[{cid}]"] = config_record(cid, world, rank, device, args)
+        if cid == 0:
+            if world == 1:  # the reference's single-process CPU case: one rank, no sharding
+                configs["configs[0]"] = config0_record(device, args)
+        else:
+            configs[f"configs[{cid}]"] = config_record(cid, world, rank, device, args)
         torch.cuda.empty_cache()
     gbuild = graph_build_time(B, N, device)
 

@@ -105,6 +105,13 @@ class GradAllReducer:
             for p in b:
                 self._bucket_of[id(p)] = bi
         self._scale = 1.0 / self.world
+        self._empty = False  # this rank holds no graphs this step (set_local_count(0))
+        #: (event, bucket) in the order they happen during a backward: ("grad", b) when a parameter's
+        #: gradient lands, ("launch", b) when a bucket's all-reduce is started; ``last_events`` is the
+        #: record of the last synchronized step — the evidence that the all-reduces overlap backward
+        #: (tests/test_dist_gloo.py)
+        self.events: List[Tuple[str, int]] = []
+        self.last_events: List[Tuple[str, int]] = []
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
         self.reset()
 
@@ -117,6 +124,9 @@ class GradAllReducer:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         total = float(t.item())
         self._scale = float(n_local) / total if total > 0 else 0.0
+        # an empty shard (more ranks than graphs, e.g. a DataLoader's short last batch) has a mean loss
+        # of 0/0 = NaN: its contribution must be exact zeros, since 0 * NaN would poison every rank
+        self._empty = n_local == 0
         return self._scale
 
     def _device(self):
@@ -125,6 +135,7 @@ class GradAllReducer:
         return torch.device("cpu")
 
     def reset(self) -> None:
+        self.events = []
         self._pending = [len(b) for b in self.buckets]
         self._work = [None] * len(self.buckets)
         self._flat = [None] * len(self.buckets)
@@ -135,6 +146,7 @@ class GradAllReducer:
             raise RuntimeError("GradAllReducer: a gradient landed after its bucket's all-reduce was launched "
                                "(more than one backward before synchronize()); call synchronize() after "
                                "every backward")
+        self.events.append(("grad", bi))
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._launch(bi)
@@ -142,7 +154,11 @@ class GradAllReducer:
     def _launch(self, bi: int) -> None:
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.buckets[bi]]
         flat = torch.cat([g.reshape(-1) for g in grads])
-        flat.mul_(self._scale)  # n_r / N (or 1 / P): the SUM all-reduce then yields the average
+        if self._empty:
+            flat.zero_()
+        else:
+            flat.mul_(self._scale)  # n_r / N (or 1 / P): the SUM all-reduce then yields the average
+        self.events.append(("launch", bi))
         self._flat[bi] = flat
         self._work[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
@@ -164,6 +180,7 @@ class GradAllReducer:
                 else:
                     p.grad.copy_(g)
                 off += n
+        self.last_events = self.events
         self.reset()
 
     def remove(self) -> None:

@@ -92,7 +92,7 @@ def edge_encoder_forward(params: Dict[str, torch.Tensor], pose: torch.Tensor) ->
     ``params`` uses the reference state_dict keys without the ``edge_encoder.`` prefix."""
     h = F.relu(F.linear(pose.float(), params["layers.0.weight"], params["layers.0.bias"]))
     out = torch.sigmoid(F.linear(h, params["layers.2.weight"], params["layers.2.bias"]))
-    return out.view(out.shape[0], -1, 2)
+    return out.view(out.shape[0], out.shape[1] // 2, 2)  # (E, C, 2); explicit C so E = 0 works
 
 
 def film_aggregate(x: torch.Tensor, gb: torch.Tensor, src, dst, mode: str = "film_mean") -> torch.Tensor:

@@ -47,12 +47,16 @@ def stack_forward(params, x, pose, src, dst, layers, combine="cat_compress", alp
     return h
 
 
-def run(params, x, pose, src, dst, grad, dtype, **kw):
-    """(output, dx, {param: grad}) of the restated stack in ``dtype``."""
+def run(params, x, pose, src, dst, grad, dtype, loss=None, **kw):
+    """(output, dx, {param: grad}) of the restated stack in ``dtype``, backpropagating ``grad``
+    (or, with ``loss="square_sum"``, the gradient of ``out.square().sum()``)."""
     p = {k: v.detach().to(dtype).requires_grad_(True) for k, v in params.items()}
     xx = x.detach().to(dtype).requires_grad_(True)
     out = stack_forward(p, xx, pose, src, dst, **kw)
-    out.backward(grad.to(dtype))
+    if loss == "square_sum":
+        out.square().sum().backward()
+    else:
+        out.backward(grad.to(dtype))
     return out.detach(), xx.grad, {k: v.grad for k, v in p.items()}
 
 

@@ -58,6 +58,49 @@ def test_unpickled_reference_gcn_warns_and_returns_input():
     assert ck["model"](g) is x  # what the reference forward returns; no kernel runs (works on the CPU)
 
 
+def _native_stack(C=32):
+    opt = types.SimpleNamespace(feature_dim=C, compress_gcn=True, multi_gcn=True)
+    torch.manual_seed(1)
+    return m.GCNStack(opt)
+
+
+def _round_trips(obj, tmp_path):
+    import copy
+    import io
+    import warnings
+    buf = io.BytesIO()
+    torch.save({"model": obj}, buf)  # the reference's whole-module checkpoint (training.py:345-355)
+    buf.seek(0)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # no "returning the input" warning for a native model
+        return [copy.deepcopy(obj), torch.load(buf, weights_only=False)["model"]]  # our own file
+
+
+def test_native_gcn_survives_deepcopy_and_checkpoint(tmp_path):
+    """A GCN built here (opt without gcn_return) keeps computing the aggregate after deepcopy and a
+    whole-module torch.save / torch.load; only a reference-pickled GCN falls back to 'input'."""
+    stack = _native_stack()
+    assert stack.gcn1._return_mode() == "aggregate"
+    for copy_ in _round_trips(stack, tmp_path):
+        assert copy_.gcn1._return_mode() == "aggregate" and copy_.gcn2._return_mode() == "aggregate"
+        assert sorted(copy_.state_dict()) == sorted(stack.state_dict())
+
+
+@pytest.mark.gpu
+def test_native_gcn_round_trip_outputs_identical(cuda_device, tmp_path):
+    stack = _native_stack().to(cuda_device)
+    rng = np.random.RandomState(4)
+    g = m.batch([m.frame_graph(np.concatenate([rng.uniform(-5, 5, (4, 3)), rng.standard_normal((4, 4))], 1)
+                               .astype(np.float32)) for _ in range(3)])
+    g.ndata["image"] = torch.randn(12, 32, 8, 8)
+    g = g.to(cuda_device)
+    with torch.no_grad():
+        ref = stack(g, g.ndata["image"])
+        assert not torch.equal(ref, g.ndata["image"][:, :32])
+        for copy_ in _round_trips(stack, tmp_path):
+            assert torch.equal(copy_.to(cuda_device)(g, g.ndata["image"]), ref)
+
+
 def test_models_alias_resolves_reference_only_names_through_fallback():
     with m.compat.reference_class_path():
         from model import models

@@ -155,3 +155,110 @@ def _accum_worker(rank, world, port):
 
 def test_second_backward_before_synchronize_raises():
     mp.spawn(_accum_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _stack_params(C, layers):
+    torch.manual_seed(9)
+    import mrp_gnn_amd as m
+    opt = type("opt", (), {"feature_dim": C, "compress_gcn": True, "multi_gcn": False, "gcn_layers": layers,
+                           "gcn_combine": "cat_compress"})()
+    return {k: v.detach().clone() for k, v in m.GCNStack(opt).named_parameters()}
+
+
+def _stack_loss(params, g, layers):
+    """mean(stack(x)^2) for a k-layer cat_compress stack with the CPU oracle per layer
+    (dgl/model/models.py:180-189 generalised): gcn_i's edge encoder and conv_i are the leaves."""
+    import oracle
+    h = g.ndata["image"]
+    src, dst = (t.numpy() for t in g.edges())
+    for i in range(1, layers + 1):
+        pre = f"gcn{i}.edge_encoder."
+        enc = {k[len(pre):]: v for k, v in params.items() if k.startswith(pre)}
+        agg = oracle.film_aggregate(h, oracle.edge_encoder_forward(enc, g.edata["pose"]), src, dst)
+        h = torch.nn.functional.conv2d(torch.cat((h, agg), 1), params[f"conv{i}.weight"], params[f"conv{i}.bias"])
+    return h.square().mean()
+
+
+def _knn_frames(B, N, C, k, seed):
+    import numpy as np
+
+    import mrp_gnn_amd as m
+    rng = np.random.RandomState(seed)
+    frames = []
+    for _ in range(B):
+        poses = np.concatenate([rng.uniform(-5, 5, (N, 3)), rng.standard_normal((N, 4))], 1).astype(np.float32)
+        f = m.frame_graph(poses, knn=k)
+        f.ndata["image"] = torch.from_numpy(rng.standard_normal((N, C, 4, 4)).astype(np.float32))
+        frames.append(f)
+    return m.batch(frames)
+
+
+def _overlap_worker(rank, world, port):
+    """configs[4]'s stack at reduced size (3 layers, k-NN(4) graphs of 16 robots, C=8): the reduced
+    gradients equal the full batch's, and backward launches a bucket's all-reduce before the last
+    parameter's gradient lands (the all-reduce overlaps the rest of backward)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mrp_gnn_amd.dist import shard_graph
+        C, L = 8, 3
+        g = _knn_frames(5, 16, C, 4, seed=21)
+        ref = {k: v.clone().requires_grad_(True) for k, v in _stack_params(C, L).items()}
+        _stack_loss(ref, g, L).backward()
+        params = {k: torch.nn.Parameter(v.clone()) for k, v in _stack_params(C, L).items()}
+        # registration order = the stack's parameter order; buckets of ~one layer's gradients
+        red = GradAllReducer(params.values(), bucket_bytes=4 * (2 * C * C + 12 * C + 2 * C * C + C))
+        assert len(red.buckets) >= 3
+        sub, (lo, hi) = shard_graph(g, rank, world)
+        red.set_local_count(hi - lo)
+        _stack_loss(params, sub, L).backward()
+        red.synchronize()
+        ev = red.last_events
+        last_grad = max(i for i, (e, _) in enumerate(ev) if e == "grad")
+        first_launch = min(i for i, (e, _) in enumerate(ev) if e == "launch")
+        assert first_launch < last_grad, ev  # a bucket went out while backward was still producing grads
+        assert sum(1 for e, _ in ev if e == "launch") == len(red.buckets)
+        for k in params:
+            assert torch.allclose(params[k].grad, ref[k].grad, rtol=1e-5, atol=1e-7), (rank, k)
+        red.remove()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_overlaps_backward_three_layer_stack():
+    mp.spawn(_overlap_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _empty_shard_worker(rank, world, port):
+    """More ranks than graphs (a DataLoader's short last batch): the empty rank's NaN mean loss must
+    not poison the reduced gradient."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mrp_gnn_amd.dist import shard_graph
+        C = 8
+        g = _frames(1, 4, C, seed=3)
+        ref = {k: v.clone().requires_grad_(True) for k, v in _gcn_params(C).items()}
+        _block_loss(ref, g).backward()
+        params = {k: torch.nn.Parameter(v.clone()) for k, v in _gcn_params(C).items()}
+        red = GradAllReducer(params.values())
+        sub, (lo, hi) = shard_graph(g, rank, world)
+        assert (hi - lo) == (1 if rank == 0 else 0)
+        red.set_local_count(hi - lo)
+        loss = _block_loss(params, sub)
+        if rank == 1:
+            assert torch.isnan(loss)  # mean over zero graphs
+        loss.backward()
+        red.synchronize()
+        for k in params:
+            assert torch.isfinite(params[k].grad).all(), (rank, k)
+            assert torch.allclose(params[k].grad, ref[k].grad, rtol=1e-5, atol=1e-7), (rank, k)
+        red.remove()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_world2_batch1_empty_shard():
+    mp.spawn(_empty_shard_worker, args=(2, _free_port()), nprocs=2, join=True)
