@@ -61,8 +61,8 @@ def run(params, x, pose, src, dst, grad, dtype, loss=None, **kw):
 
 
 def err(a, ref):
-    a = a.detach().double()
-    ref = ref.detach().double()
+    a = a.detach().double().cpu()
+    ref = ref.detach().double().cpu()
     return float((a - ref).abs().max() / ref.abs().max().clamp_min(1e-300))
 
 

@@ -31,7 +31,7 @@ def test_hidden_kernel_vs_torch(cuda_device, E, C):
     l1 = enc.layers[0]
     h = m.encoder.hidden_forward(pose, l1.weight, l1.bias)
     ref = torch.relu(l1(pose))
-    assert float((h - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
+    assert float((h - ref).detach().abs().max()) <= 1e-5 * max(1.0, float(ref.detach().abs().max()))
     # the full logits path and its backward vs torch autograd through the reference layers
     g = torch.randn(E, 2 * C, device=cuda_device)
     pr = pose.clone().requires_grad_(True)
