@@ -195,10 +195,8 @@ int mrp_film_mean_fwd_ex(const float* x, int64_t x_node_stride,
                          void* stream);
 
 /* mrp_film_mean_bwd for a forward run with `epilogue` (NULL: plain; see mrp_agg_epilogue).
- * workspace: optional device scratch of workspace_bytes >= mrp_film_mean_bwd_workspace(...) bytes
- * (NULL/0 allowed).  For MRP_GRAPH_REGULAR graphs of more than 8 nodes it lets the backward split
- * each channel plane over several workgroups and reduce their partial d gamma/beta sums in a second
- * pass (fixed order: deterministic); without it each plane is one workgroup. */
+ * workspace: reserved (NULL/0 allowed; mrp_film_mean_bwd_workspace returns 0): ABI 11's plane-split
+ * k-NN backward that used it measured slower than whole planes and was removed in ABI 12. */
 int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride,
                          const float* x, int64_t x_node_stride,
                          const float* gb,
@@ -213,7 +211,8 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride,
                          void* workspace, int64_t workspace_bytes,
                          void* stream);
 
-/* Bytes of workspace mrp_film_mean_bwd_ex can use for these graph/feature sizes (0: none needed). */
+/* Bytes of workspace mrp_film_mean_bwd_ex can use for these graph/feature sizes (0: none needed;
+ * always 0 since ABI 12). */
 int64_t mrp_film_mean_bwd_workspace(int32_t num_graphs, int32_t max_nodes, int32_t graph_kind,
                                     int32_t C, int32_t P);
 
@@ -298,7 +297,9 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * "bwd_fused_*", "bwd_regular_*"; kernel choice: "bwd_regular_mfma" (1, default: the matrix-core
  * backward for MRP_GRAPH_REGULAR graphs of 9..16 nodes), "bwd_complete_mfma" (0, default: complete
  * graphs keep the VALU backward), "bwd_mfma_cpw" (channel blocks per wave of the matrix-core
- * backward, 1 or 2), "bwd_pre2", "fwd_regular_split" (0, default: whole planes). */
+ * backward, 1 or 2), "bwd_pre2", "fwd_regular_split" (0, default: whole planes); compress GEMM
+ * kernel variants "gemm_nn" / "gemm_nt" (-1, default: the per-shape choice; 0..5: compress_gemm.hip's
+ * variant table). */
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 12 = this header: the

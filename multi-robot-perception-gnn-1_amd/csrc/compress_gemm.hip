@@ -73,10 +73,10 @@ struct Cfg {
 // variant table (mrp_tuning_set "gemm_nn" / "gemm_nt"; -1 = the default, V1)
 using V0 = Cfg<16, 32, 2, 2, 2>;  // 128 x 128, 64 KiB: two workgroups per CU
 using V1 = Cfg<32, 32, 2, 2, 2>;  // the same on 32x32x2 MFMAs
-using V2 = Cfg<16, 32, 2, 4, 2>;  // 256 x 128, 96 KiB
-using V3 = Cfg<32, 32, 2, 4, 2>;  // the same on 32x32x2 MFMAs
-using V4 = Cfg<32, 64, 2, 2, 2>;  // 64-deep stages, 128 KiB
-using V5 = Cfg<32, 32, 2, 2, 4>;  // 128 x 256, 96 KiB
+using V2 = Cfg<16, 32, 3, 2, 2>;  // three buffers (96 KiB): one workgroup per CU, two stages in flight
+using V3 = Cfg<32, 32, 3, 2, 2>;  // the same on 32x32x2 MFMAs
+using V4 = Cfg<32, 32, 4, 2, 2>;  // four buffers (128 KiB), three stages in flight
+using V5 = Cfg<32, 32, 2, 4, 2>;  // 256 x 128, 96 KiB
 #define MRP_CG_VARIANTS(X) X(0, V0) X(1, V1) X(2, V2) X(3, V3) X(4, V4) X(5, V5)
 constexpr int kVariants = 6;
 
@@ -113,21 +113,42 @@ __device__ __forceinline__ int swz_a(int row) {
 // then stage s + 1's first fragments are read under stage s's last MFMA group.  One barrier per
 // stage and no LDS latency exposed after it.  The loop is unrolled by 2 so every LDS offset is an
 // immediate.  issue(stage, buf), read(buf, g, frags), mma(frags).
+// With NBUF > 2, NBUF - 1 stages are in flight: the wait before the barrier leaves the younger
+// stages' pieces outstanding (counted vmcnt) and the barrier is the raw s_barrier (__syncthreads()
+// would wait vmcnt(0) and drain them); stage s + NBUF - 1 goes into buffer s % NBUF.
+template <class G>
+__device__ __forceinline__ void stage_barrier(int younger) {  // younger: stages issued after the one waited for
+  if constexpr (G::NBUF == 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    if (younger >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (G::PA + G::PB)) : "memory");
+    else if (younger == 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PA + G::PB) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
 template <class G, class Issue, class Read, class Mma>
 __device__ __forceinline__ void kloop(int nst, Issue&& issue, Read&& read, Mma&& mma) {
-  static_assert(G::NBUF == 2, "kloop: two LDS buffers");
+  constexpr int NB = G::NBUF;
+  static_assert(NB >= 2 && NB <= 4, "kloop: 2 to 4 LDS buffers");
   constexpr int NG = G::BK / 16;
   typedef float Frag[2][G::FB][G::T];  // [A | B][block][k-step]
   Frag f[2];
   if (nst <= 0) return;
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (nst > 1) issue(1, 1);
-  read(0, 0, f[0]);
-  for (int s0 = 0; s0 < nst; s0 += 2) {
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+  for (int p = 0; p < NB - 1; ++p)
+    if (p < nst) issue(p, p);
+  stage_barrier<G>(min(NB - 2, nst - 1));
+  read(0, 0, f[0]);
+  for (int s0 = 0; s0 < nst; s0 += NB) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
       const int s = s0 + b;
       if (s < nst) {
 #pragma unroll
@@ -135,10 +156,9 @@ __device__ __forceinline__ void kloop(int nst, Issue&& issue, Read&& read, Mma&&
           if (g + 1 < NG) {
             read(b, g + 1, f[(g + 1) & 1]);
           } else if (s + 1 < nst) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (s + 2 < nst) issue(s + 2, b);
-            read(1 - b, 0, f[(g + 1) & 1]);
+            stage_barrier<G>(min(NB - 2, nst - 2 - s));  // stages issued after s + 1
+            if (s + NB - 1 < nst) issue(s + NB - 1, (b + NB - 1) % NB);
+            read((b + 1) % NB, 0, f[(g + 1) & 1]);
           }
           mma(f[g & 1]);
         }

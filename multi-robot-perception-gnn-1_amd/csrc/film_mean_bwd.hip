@@ -14,19 +14,6 @@ Geometry regular_geometry(int C, int P, int vec) {
                   : make_geometry(C, P, 1, 2 * tu.bwd_regular_lanes, 2 * tu.bwd_regular_lanes, mrp::kMaxChanPerBlock);
 }
 
-// Plane segments of the split regular backward: each lane owns tu.bwd_regular_slices slices.
-int regular_psplit(const Geometry& g, int P) {
-  const int spl = tuning().bwd_regular_slices;
-  if (spl <= 0) return 1;
-  const int per_lane = (P / g.vec + g.lpc - 1) / g.lpc;
-  return std::max(1, per_lane / spl);
-}
-
-int64_t regular_ws_bytes(const Geometry& g, int num_graphs, int nt, int kmax, int psplit) {
-  return psplit <= 1 ? 0
-                     : (int64_t)num_graphs * g.ncb * psplit * g.cpb * (nt * kmax + nt) * (int64_t)sizeof(float);
-}
-
 hipError_t dispatch_bwd(int nt, bool complete, const AggArgs& a, const Geometry& g, hipStream_t st) {
   if (nt >= 1 && nt <= 8) return dispatch_bwd_1_8(nt, complete, a, g, st);
   if (nt >= 9 && nt <= 12) return dispatch_bwd_9_12(nt, complete, a, g, st);
@@ -49,18 +36,10 @@ int mrp_film_mean_bwd(const float* grad_out, int64_t g_node_stride, const float*
                               grad_x_base, base_node_stride, grad_gb, nullptr, nullptr, 0, stream);
 }
 
-int64_t mrp_film_mean_bwd_workspace(int32_t num_graphs, int32_t max_nodes, int32_t graph_kind, int32_t C, int32_t P) {
-  const int kdeg = MRP_GRAPH_IS_REGULAR(graph_kind) ? MRP_GRAPH_REGULAR_K(graph_kind) : 0;
-  if (num_graphs <= 0 || max_nodes <= 8 || max_nodes > MRP_MAX_NODES || kdeg < 1 || kdeg > 8 || C <= 0 || P <= 0)
-    return 0;
-  const int kmax = kdeg <= 4 ? 4 : 8;
-  int64_t bytes = 0;
-  for (int vec : {1, 2}) {  // the launch picks the slice width from pointer alignment: cover both
-    const Geometry g = regular_geometry(C, P, vec);
-    bytes = std::max(bytes, regular_ws_bytes(g, num_graphs, max_nodes, kmax, regular_psplit(g, P)));
-  }
-  return bytes;
-}
+// No backward kernel of this library version needs scratch (the plane-split k-NN backward that used
+// it measured slower and is gone, round 3); kept so callers written against the workspace
+// contract keep working.
+int64_t mrp_film_mean_bwd_workspace(int32_t, int32_t, int32_t, int32_t, int32_t) { return 0; }
 
 int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const float* x, int64_t x_node_stride,
                          const float* gb, const int32_t* indptr, const int32_t* src, const int32_t* eid,
@@ -116,18 +95,13 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const flo
   } else {
     g = make_geometry(C, P, vec, 64, 64, mrp::kMaxChanPerBlock);  // film_bwd_dx + Gram pass
   }
-  // REGULAR (k-NN) graphs with a large enough caller workspace: planes split over several workgroups,
-  // partial Grams reduced by a second kernel (film_bwd_regular_reduce)
-  int psplit = 1;
-  if (max_nodes > 8 && kdeg >= 1 && kdeg <= 8 && want_dgb && workspace != nullptr) {
-    const int ps = regular_psplit(g, P);
-    if (ps > 1 && regular_ws_bytes(g, num_graphs, max_nodes, kdeg <= 4 ? 4 : 8, ps) <= workspace_bytes) psplit = ps;
-  }
+  (void)workspace;
+  (void)workspace_bytes;
   // film_bwd_mfma: regular graphs of 9..16 nodes and complete graphs, whole pixel groups of 64
   const bool complete = graph_kind == MRP_GRAPH_COMPLETE;
   const bool mfma_kind = (max_nodes > 8 && kdeg >= 1 && kdeg <= 8 && tuning().bwd_regular_mfma) ||
                          (complete && max_nodes >= 2 && tuning().bwd_complete_mfma);
-  if (mfma_kind && psplit == 1 && vec4 && P % 64 == 0) {
+  if (mfma_kind && vec4 && P % 64 == 0) {
     // per-lane row offsets are 32-bit: 15 node strides + two planes (a block's channel pair)
     const int64_t lim = (int64_t)1 << 32;
     const int64_t span = (int64_t)plane * 4 + (int64_t)P * 4;
@@ -145,7 +119,7 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const flo
       g.ncb = (C + g.cpb - 1) / g.cpb;
     }
   }
-  g.grid = (int64_t)num_graphs * g.ncb * psplit;
+  g.grid = (int64_t)num_graphs * g.ncb;
   if (g.grid > 0x7fffffff) return hipErrorInvalidValue;
   AggArgs a = {};
   a.x = x;
@@ -176,8 +150,7 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const flo
   a.agg_scale = agg_scale;
   a.self_scale = self_scale;
   a.epi = (agg_scale != 1.f || self_scale != 0.f) ? 1 : 0;
-  a.psplit = psplit;
-  a.ws = psplit > 1 ? static_cast<float*>(workspace) : nullptr;
+  a.psplit = 1;
   a.nmax = max_nodes;
   return dispatch_bwd(max_nodes, graph_kind == MRP_GRAPH_COMPLETE, a, g, st);
 }

@@ -62,11 +62,6 @@ hipError_t launch_bwd_regular(const AggArgs& a, const Geometry& g, hipStream_t s
     }
   }
   if (!done) MRP_LAUNCH((mrp::film_bwd_regular<NT, KMAX, 1, DXB>), lds);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || a.psplit <= 1 || !a.want_dgb) return e;
-  // plane-split: add the segments' partial Grams (one workgroup per graph x channel block)
-  hipLaunchKernelGGL((mrp::film_bwd_regular_reduce<NT, KMAX>), dim3((unsigned)(g.grid / a.psplit)), dim3(mrp::kBlock), 0,
-                     st, a);
   return hipGetLastError();
 }
 

@@ -100,7 +100,6 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"bwd_pre2", &t.bwd_pre2, 0, 1},
       {"bwd_regular_vec", &t.bwd_regular_vec, 1, 2},
       {"bwd_regular_lanes", &t.bwd_regular_lanes, 1, 64},
-      {"bwd_regular_slices", &t.bwd_regular_slices, 0, 64},
       {"bwd_regular_mfma", &t.bwd_regular_mfma, 0, 1},
       {"bwd_complete_mfma", &t.bwd_complete_mfma, 0, 1},
       {"bwd_mfma_cpw", &t.bwd_mfma_cpw, 1, 2},

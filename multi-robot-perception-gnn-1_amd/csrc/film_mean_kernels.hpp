@@ -80,8 +80,6 @@ struct AggArgs {
   float agg_scale, self_scale, x0_scale;
   const float* x0;
   int64_t x0s;
-  // backward of REGULAR graphs with psplit > 1: per-segment partial Grams, [graph][cb][seg][cpb][NS + NT]
-  float* ws;
   int32_t nmax;  // max_nodes (COMPLETE graphs: every graph's node count)
 };
 
@@ -1176,17 +1174,13 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
   int* slot_u = reinterpret_cast<int*>(sc + NTP);  // [NS] local source of slot (v, j)
   int* slot_e = slot_u + NS;                       // [NS] edge id of slot (v, j)
 
-  // psplit > 1: the plane is cut into segments, one workgroup each (4x the workgroups of whole
-  // planes, 2 slices per lane); each writes its partial Gram to a.ws and film_bwd_regular_reduce adds
-  // the segments in order (deterministic).  psplit == 1: the epilogue below writes d gamma/beta.
-  const int ps = a.psplit > 1 ? a.psplit : 1;
-  const int item = blockIdx.x / ps;
-  const int seg = blockIdx.x - item * ps;
-  const int b = item / a.ncb;
-  const int cb = item - b * a.ncb;
-  const int seglen = (a.PV + ps - 1) / ps;
-  const int jbeg = seg * seglen;
-  const int jend = min(a.PV, jbeg + seglen);
+  // one workgroup per (graph, channel block), whole planes (a plane split over several workgroups
+  // with a second pass adding their partial Grams measured slower at the configs[4] shape: 113-170
+  // vs 102.7 us, round 2 — each extra workgroup repeats the prologue of dependent loads)
+  const int b = blockIdx.x / a.ncb;
+  const int cb = blockIdx.x - b * a.ncb;
+  const int jbeg = 0;
+  const int jend = a.PV;
   const int node0 = a.goff[b];
   const int n = min(a.goff[b + 1] - node0, NT);
   if (n <= 0) return;
@@ -1389,16 +1383,6 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
     }
   }
   __syncthreads();
-  if (ps > 1) {
-    // partial Gram of this segment: [cpb][NS] then [cpb][NT], coalesced
-    float* w = a.ws + (int64_t)blockIdx.x * a.cpb * (NS + NT);
-    for (int t = threadIdx.x; t < a.cpb * NS; t += blockDim.x) w[t] = Dl[t];
-    for (int t = threadIdx.x; t < a.cpb * NT; t += blockDim.x) {
-      const int cl = t / NT, v = t - cl * NT;
-      w[a.cpb * NS + t] = Sl[cl * NTP + v];
-    }
-    return;
-  }
   // per-edge outputs: thread -> (channel fastest, slot)
   for (int t = threadIdx.x; t < a.cpb * NS; t += blockDim.x) {
     int cl, slot;
@@ -1410,46 +1394,6 @@ __global__ void __launch_bounds__(kBlock) film_bwd_regular(AggArgs a) {
     const float s = sc[v];
     const int64_t off = ((int64_t)e * a.C + cc) * 2;
     float2 r = make_float2(s * Dl[cl * NS + slot], s * Sl[cl * NTP + v]);
-    if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
-    *reinterpret_cast<float2*>(a.dgb + off) = r;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Second pass of the plane-split REGULAR backward: per (graph, channel block), add the psplit
-// partial Grams in segment order and write d gamma / d beta for every (edge slot, channel) —
-// the psplit == 1 epilogue of film_bwd_regular, reading partials from a.ws instead of LDS.
-// ---------------------------------------------------------------------------
-template <int NT, int KMAX>
-__global__ void __launch_bounds__(kBlock) film_bwd_regular_reduce(AggArgs a) {
-  constexpr int NS = NT * KMAX;
-  const int b = blockIdx.x / a.ncb;
-  const int cb = blockIdx.x - b * a.ncb;
-  const int node0 = a.goff[b];
-  const int n = min(a.goff[b + 1] - node0, NT);
-  if (n <= 0) return;
-  const int c0 = cb * a.cpb;
-  const int K = a.kdeg;
-  const int ps = a.psplit;
-  const float s = (a.mode != MRP_AGG_FILM_SUM ? 1.f / (float)K : 1.f) * a.agg_scale;
-  const float* w0 = a.ws + (int64_t)blockIdx.x * ps * a.cpb * (NS + NT);
-  for (int t = threadIdx.x; t < a.cpb * NS; t += blockDim.x) {
-    int cl, slot;
-    split_channel(a, t, cl, slot);
-    const int v = slot / KMAX, jj = slot - v * KMAX;
-    const int cc = c0 + cl;
-    if (v >= n || jj >= K || cc >= a.C) continue;
-    const int k = (node0 + v) * K + jj;  // REGULAR: v's CSR row is [K*v, K*(v+1))
-    const int u = a.src[k] - node0;
-    if ((unsigned)u >= (unsigned)n) continue;  // leaves the graph: rejected on the host
-    float dd = 0.f, ss = 0.f;
-    for (int sg = 0; sg < ps; ++sg) {
-      const float* w = w0 + (int64_t)sg * a.cpb * (NS + NT);
-      dd += w[cl * NS + slot];
-      ss += w[a.cpb * NS + cl * NT + v];
-    }
-    const int64_t off = ((int64_t)a.eid[k] * a.C + cc) * 2;
-    float2 r = make_float2(s * dd, s * ss);
     if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
     *reinterpret_cast<float2*>(a.dgb + off) = r;
   }

@@ -25,12 +25,6 @@ struct Tuning {
   int bwd_regular_mfma = 1;
   int bwd_complete_mfma = 0;
   int bwd_mfma_cpw = 2;  // film_bwd_mfma: 16-row blocks per wave (1 or 2)
-  // film_bwd_regular: split planes so each lane owns this many slices (0: whole planes); needs the
-  // caller's workspace (mrp_film_mean_bwd_workspace), else whole planes.  Measured slower at the
-  // configs[4] shape (k-NN(4) N=16 C=1024 16x16 B=8: 102.7 us whole planes, 113 / 131 / 170 us at
-  // 4 / 2 / 1 slices per lane): each extra workgroup repeats a prologue of dependent loads that the
-  // 2-waves-per-SIMD kernel cannot hide.  Off by default; kept as a tested experiment path.
-  int bwd_regular_slices = 0;
 
   // compress GEMMs (compress_gemm.hip): kernel variant of the forward / data-gradient product (NN) and
   // of the weight-gradient product (NT); see the variant table there

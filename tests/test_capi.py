@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r"\bT (mrp_\w+)$", out, re.M))
-    assert declared_symbols() <= exported
+    assert declared_symbols() == exported  # exactly the header's entry points: no lab hooks
 
 
 def test_library_targets_gfx950_only():
@@ -105,6 +105,7 @@ def test_frame_batch_needs_the_gpu():
 def test_edge_encoder_bwd_validation_without_launch():
     lib = m.load_library()
     assert lib.mrp_edge_encoder_bwd_workspace(1792, 512) == 112 * 12 * 512 * 4  # 16-edge chunks x 12C floats
+    assert lib.mrp_film_mean_bwd_workspace(8, 16, m.graph_regular(4), 1024, 256) == 0  # reserved since ABI 12
     assert lib.mrp_edge_encoder_bwd_workspace(0, 512) == 0
     assert lib.mrp_edge_encoder_bwd(None, None, None, None, -1, 4, None, None, None, None, None) == HIP_INVALID_VALUE
     # work to do but a missing input or workspace
@@ -118,7 +119,8 @@ def test_tuning_knobs_documented_in_the_header():
     lib = m.load_library()
     try:
         for name, lo, hi in (("bwd_regular_mfma", 0, 1), ("bwd_complete_mfma", 0, 1), ("bwd_mfma_cpw", 1, 2),
-                             ("bwd_pre2", 0, 1), ("fwd_regular_split", 0, 1), ("bwd_fused_cap", 1, 64)):
+                             ("bwd_pre2", 0, 1), ("fwd_regular_split", 0, 1), ("bwd_fused_cap", 1, 64),
+                             ("gemm_nn", -1, 5), ("gemm_nt", -1, 5)):
             assert name.encode() in open(os.path.join(ROOT, "include", "mrp_gnn.h"), "rb").read() or \
                 name.startswith("bwd_fused")
             assert lib.mrp_tuning_set(name.encode(), lo) == 0

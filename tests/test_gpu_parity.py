@@ -466,35 +466,6 @@ def test_cat_forward_strided_source(cuda_device):
     assert torch.equal(buf.cpu(), ref)
 
 
-@pytest.mark.parametrize("slices", [1, 2])
-def test_regular_backward_plane_split_path(cuda_device, slices):
-    """The plane-split k-NN backward (partial Grams in a caller workspace + film_bwd_regular_reduce),
-    an experiment knob that is off by default: same gradients as the whole-plane kernel."""
-    lib = m.load_library()
-    g, x, gb = random_case(16, 24, 16, 16, seed=3, knn=4, bnn=[16, 16, 13])
-    csr = g.csr(cuda_device)
-    assert csr.graph_kind == m.graph_regular(4)
-    G = torch.randn_like(x)
-    res = []
-    try:
-        # against the whole-plane VALU kernel (the matrix-core kernel sums in another order)
-        assert lib.mrp_tuning_set(b"bwd_regular_mfma", 0) == 0
-        for knob in (0, slices):
-            assert lib.mrp_tuning_set(b"bwd_regular_slices", knob) == 0
-            xd = x.to(cuda_device).requires_grad_(True)
-            gbd = gb.to(cuda_device).requires_grad_(True)
-            m.film_mean(xd, gbd, csr, logits=True).backward(G.to(cuda_device))
-            res.append((xd.grad.cpu(), gbd.grad.cpu()))
-    finally:
-        lib.mrp_tuning_set(b"reset", 0)
-    assert torch.equal(res[0][0], res[1][0])  # dx does not depend on the split
-    assert rel_err(res[1][1].numpy(), res[0][1].numpy()) <= 1e-6
-    src, dst = (t.numpy() for t in g.edges())
-    _, dgb_ref = oracle.film_aggregate_grads(x, torch.sigmoid(gb), src, dst, G)
-    dz_ref = dgb_ref * torch.sigmoid(gb) * (1 - torch.sigmoid(gb))
-    assert rel_err(res[1][1].numpy(), dz_ref.numpy()) <= TOL
-
-
 @pytest.mark.parametrize("n,C,hw,knn", [(8, 23, (8, 8), None), (5, 16, (16, 16), None), (12, 9, (8, 8), None),
                                          (16, 13, (8, 8), 4), (11, 6, (16, 16), 6)])
 @pytest.mark.parametrize("combine", ["cat", "residual"])

@@ -176,8 +176,7 @@ def main():
         sweep("bwd", "cfg3", bwd_time, {"bwd_fused_cap": [1, 2, 4, 8]})
         return
     if what == "regbwd":
-        sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [1, 2], "bwd_regular_lanes": [8, 16, 32],
-                                        "bwd_regular_slices": [0, 1, 2, 4]})
+        sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [1, 2], "bwd_regular_lanes": [8, 16, 32]})
         for name in ("cfg2", "cfg3", "cfg1"):
             sweep("bwd", name, bwd_time, {"bwd_fused_cap": [8]})
             sweep("fwd", name, fwd_time, {"fwd_cap": [16]})
@@ -194,8 +193,7 @@ def main():
                                           "bwd_fused_cap": [8, 16, 32, 64]})
         sweep("bwd", "cfg1", bwd_time, {"bwd_fused_lo": [32, 64], "bwd_fused_hi": [64, 128, 256],
                                         "bwd_fused_cap": [2, 4, 8]})
-        sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [1, 2], "bwd_regular_lanes": [8, 16, 32],
-                                        "bwd_regular_slices": [0, 1, 2, 4]})
+        sweep("bwd", "cfg4", bwd_time, {"bwd_regular_vec": [1, 2], "bwd_regular_lanes": [8, 16, 32]})
 
 
 if __name__ == "__main__":
