@@ -295,8 +295,8 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * not thread-safe).  Returns hipErrorInvalidValue for an unknown name or a value out of range;
  * "reset" restores every default.  Geometry: "fwd_lo"/"fwd_hi"/"fwd_cap", "fwd_regular_*",
  * "bwd_fused_*", "bwd_regular_*"; kernel choice: "bwd_regular_mfma" (1, default: the matrix-core
- * backward for MRP_GRAPH_REGULAR graphs of 9..16 nodes), "bwd_complete_mfma" (0, default: complete
- * graphs keep the VALU backward), "bwd_mfma_cpw" (channel blocks per wave of the matrix-core
+ * backward for MRP_GRAPH_REGULAR graphs of 9..16 nodes), "bwd_complete_mfma" (1, default: the
+ * matrix-core backward for complete graphs of 9..16 nodes too; those of <= 8 always run the VALU one), "bwd_mfma_cpw" (channel blocks per wave of the matrix-core
  * backward, 1 or 2), "bwd_pre2", "fwd_regular_split" (0, default: whole planes); compress GEMM
  * kernel variants "gemm_nn" / "gemm_nt" (-1, default: the per-shape choice; 0..5: compress_gemm.hip's
  * variant table). */

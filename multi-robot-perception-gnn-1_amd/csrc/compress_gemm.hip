@@ -113,24 +113,23 @@ __device__ __forceinline__ int swz_a(int row) {
 // then stage s + 1's first fragments are read under stage s's last MFMA group.  One barrier per
 // stage and no LDS latency exposed after it.  The loop is unrolled by 2 so every LDS offset is an
 // immediate.  issue(stage, buf), read(buf, g, frags), mma(frags).
-// With NBUF > 2, NBUF - 1 stages are in flight: the wait before the barrier leaves the younger
-// stages' pieces outstanding (counted vmcnt) and the barrier is the raw s_barrier (__syncthreads()
-// would wait vmcnt(0) and drain them); stage s + NBUF - 1 goes into buffer s % NBUF.
+// Stages in flight: the prologue issues stages 0 .. NBUF-1 (one per buffer); at stage s's barrier
+// buffer s % NBUF has been read by every wave, so stage s + NBUF is issued into it.  The wait before
+// a barrier retires the stage it publishes and leaves the younger ones outstanding (counted vmcnt),
+// and the barrier is the raw s_barrier (__syncthreads() would wait vmcnt(0) and drain them).
 template <class G>
 __device__ __forceinline__ void stage_barrier(int younger) {  // younger: stages issued after the one waited for
-  if constexpr (G::NBUF == 2) {
+  constexpr int PS = G::PA + G::PB;  // LDS-DMA pieces per wave per stage
+  if (younger >= 3)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PS) : "memory");
+  else if (younger == 2)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PS) : "memory");
+  else if (younger == 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PS) : "memory");
+  else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  } else {
-    if (younger >= 2)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (G::PA + G::PB)) : "memory");
-    else if (younger == 1)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PA + G::PB) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 }
 
 template <class G, class Issue, class Read, class Mma>
@@ -142,9 +141,9 @@ __device__ __forceinline__ void kloop(int nst, Issue&& issue, Read&& read, Mma&&
   Frag f[2];
   if (nst <= 0) return;
 #pragma unroll
-  for (int p = 0; p < NB - 1; ++p)
+  for (int p = 0; p < NB; ++p)
     if (p < nst) issue(p, p);
-  stage_barrier<G>(min(NB - 2, nst - 1));
+  stage_barrier<G>(min(NB - 1, nst - 1));  // stage 0 landed; stages 1 .. NB-1 may still be in flight
   read(0, 0, f[0]);
   for (int s0 = 0; s0 < nst; s0 += NB) {
 #pragma unroll
@@ -156,8 +155,8 @@ __device__ __forceinline__ void kloop(int nst, Issue&& issue, Read&& read, Mma&&
           if (g + 1 < NG) {
             read(b, g + 1, f[(g + 1) & 1]);
           } else if (s + 1 < nst) {
-            stage_barrier<G>(min(NB - 2, nst - 2 - s));  // stages issued after s + 1
-            if (s + NB - 1 < nst) issue(s + NB - 1, (b + NB - 1) % NB);
+            stage_barrier<G>(min(NB - 2, nst - 2 - s));  // stage s + 1 landed; s + 2 .. s + NB - 1 in flight
+            if (s + NB < nst) issue(s + NB, b);  // into the buffer stage s just vacated
             read((b + 1) % NB, 0, f[(g + 1) & 1]);
           }
           mma(f[g & 1]);

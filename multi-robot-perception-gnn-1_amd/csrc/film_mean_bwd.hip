@@ -100,7 +100,7 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const flo
   // film_bwd_mfma: regular graphs of 9..16 nodes and complete graphs, whole pixel groups of 64
   const bool complete = graph_kind == MRP_GRAPH_COMPLETE;
   const bool mfma_kind = (max_nodes > 8 && kdeg >= 1 && kdeg <= 8 && tuning().bwd_regular_mfma) ||
-                         (complete && max_nodes >= 2 && tuning().bwd_complete_mfma);
+                         (complete && max_nodes > 8 && tuning().bwd_complete_mfma);
   if (mfma_kind && vec4 && P % 64 == 0) {
     // per-lane row offsets are 32-bit: 15 node strides + two planes (a block's channel pair)
     const int64_t lim = (int64_t)1 << 32;
@@ -111,7 +111,7 @@ int mrp_film_mean_bwd_ex(const float* grad_out, int64_t g_node_stride, const flo
     if (want_dgb) fits = fits && (int64_t)15 * x_node_stride * 4 + span < lim;
     if (fits) {
       const int cpw = tuning().bwd_mfma_cpw >= 2 ? 2 : 1;  // instantiated: 1, 2
-      g.mfma_npb = max_nodes <= 8 && complete ? 8 : 16;
+      g.mfma_npb = 16;
       g.vec = 4;
       g.lpc = 64;
       g.cpb = 4 * cpw * (16 / g.mfma_npb);  // 4 waves x blocks per wave x channels per block

@@ -89,10 +89,8 @@ hipError_t launch_bwd_mfma_k(const AggArgs& a, const Geometry& g, hipStream_t st
 template <int NT, bool COMPLETE>
 hipError_t launch_bwd_mfma(const AggArgs& a, const Geometry& g, hipStream_t st) {
   if constexpr (COMPLETE) {
-    if constexpr (NT <= 8)
-      return launch_bwd_mfma_k<true, 8, 1>(a, g, st);
-    else
-      return launch_bwd_mfma_k<true, 16, 1>(a, g, st);
+    if constexpr (NT > 8) return launch_bwd_mfma_k<true, 16, 1>(a, g, st);
+    return hipErrorInvalidValue;  // complete graphs of <= 8 nodes run film_bwd_fused
   } else {
     if constexpr (NT > 8) {
       if (a.kdeg >= 1 && a.kdeg <= 4) return launch_bwd_mfma_k<false, 16, 4>(a, g, st);

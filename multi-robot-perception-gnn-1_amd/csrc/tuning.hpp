@@ -19,11 +19,14 @@ struct Tuning {
   int bwd_fused_lo = 8, bwd_fused_hi = 128, bwd_fused_cap = 16;
   int bwd_pre2 = 1;  // film_bwd_fused: prefetch both slices when a lane owns exactly two
   int bwd_regular_vec = 2, bwd_regular_lanes = 16;              // film_bwd_regular (N > 8, k-NN)
-  // film_bwd_mfma (Gram and grad_x on the matrix cores; P % 64 == 0, 16-byte aligned operands):
-  // regular graphs of 9..16 nodes (0 = film_bwd_regular), complete graphs (1; default 0: film_bwd_fused
-  // measured faster at every config: 143 vs 159 us at configs[1], 59 vs 64 at [2], 27 vs 29 at [3])
+  // film_bwd_mfma (Gram and grad_x on the matrix cores; P % 64 == 0, 16-byte aligned operands) for
+  // graphs of 9..16 nodes: regular (k-NN; 0 = film_bwd_regular) and complete (0 = film_bwd_dx + the
+  // Gram pass: 239.9 vs 90.5 us at B=8 N=16 C=1024 16x16, 65.1 vs 49.4 at B=32 N=12 C=512 8x8,
+  // tools/exp_bwd_complete16.py).  Complete graphs of <= 8 nodes keep film_bwd_fused (the matrix-core
+  // form, two channels per 16-row block, measured slower there: 30.9 vs 25.7 us at configs[3],
+  // 159 vs 143 at [1]; removed in round 3)
   int bwd_regular_mfma = 1;
-  int bwd_complete_mfma = 0;
+  int bwd_complete_mfma = 1;
   int bwd_mfma_cpw = 2;  // film_bwd_mfma: 16-row blocks per wave (1 or 2)
 
   // compress GEMMs (compress_gemm.hip): kernel variant of the forward / data-gradient product (NN) and

@@ -470,8 +470,8 @@ def test_cat_forward_strided_source(cuda_device):
                                          (16, 13, (8, 8), 4), (11, 6, (16, 16), 6)])
 @pytest.mark.parametrize("combine", ["cat", "residual"])
 def test_mfma_backward_matches_valu_kernels(cuda_device, n, C, hw, knn, combine):
-    """film_bwd_mfma (Gram and grad_x on the matrix cores; the default for k-NN graphs of 9..16 nodes,
-    an opt-in for complete graphs) against the VALU kernels (film_bwd_fused / film_bwd_regular) and the
+    """film_bwd_mfma (Gram and grad_x on the matrix cores; the default for k-NN and complete graphs of
+    9..16 nodes; graphs of <= 8 nodes run the VALU kernel either way) against the VALU kernels (film_bwd_fused / film_bwd_regular) and the
     oracle: odd channel counts (a channel pair with one channel past C), graphs of 5..16 nodes, the
     cat backward's grad_x base and the residual epilogue's self term."""
     lib = m.load_library()
