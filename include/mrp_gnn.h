@@ -218,7 +218,7 @@ int64_t mrp_film_mean_bwd_workspace(int32_t num_graphs, int32_t max_nodes, int32
 
 /*
  * The layer's 1x1 compress convolution and its gradients, fp32 on the matrix cores (exact fp32
- * products, v_mfma_f32_16x16x4_f32), without the concatenation (dgl/model/models.py:163-165,181-184,
+ * products, v_mfma_f32_32x32x2_f32), without the concatenation (dgl/model/models.py:163-165,181-184,
  * 186-189: h = conv(torch.cat((x, a), 1)) with conv = nn.Conv2d(2C, C, kernel_size=1)).  W is the
  * conv weight (C, 2C) row-major (nn.Conv2d's (C, 2C, 1, 1)); x and a are the two halves of the
  * concatenation as separate node-major tensors (any node strides, e.g. the two halves of one cat
@@ -249,11 +249,21 @@ int mrp_compress_bwd_weight(const float* gy, int64_t gy_node_stride, const float
 /*
  * First layer of the edge encoder, dgl/model/models.py:147-148:  h = relu(pose W1^T + b1).
  *   pose (num_edges, 9), w1 (C, 9) (nn.Linear weight layout), b1 (C) -> h (num_edges, C), fp32.
- * The second Linear is a plain library GEMM and its Sigmoid is fused into the aggregation
+ * The second Linear is mrp_edge_logits_fwd and its Sigmoid is fused into the aggregation
  * (MRP_AGG_GB_LOGITS).
  */
 int mrp_edge_hidden_fwd(const float* pose, const float* w1, const float* b1,
                         int32_t num_edges, int32_t C, float* h, void* stream);
+
+/*
+ * Second layer of the edge encoder before its Sigmoid, dgl/model/models.py:149:
+ *   z = h W2^T + b2,  h (num_edges, C), w2 (2C, C) (nn.Linear weight layout), b2 (2C) -> z (num_edges, 2C)
+ * fp32 on the matrix cores (exact fp32 products), the bias added in the epilogue.  z is the logits
+ * tensor the aggregation reads with MRP_AGG_GB_LOGITS.  Requirements (else hipErrorNotSupported):
+ * C % 32 == 0, h and w2 16-byte aligned, h and w2 under 2^31 bytes.
+ */
+int mrp_edge_logits_fwd(const float* h, int32_t num_edges, int32_t C, const float* w2, const float* b2,
+                        float* z, void* stream);
 
 /*
  * Backward of the edge encoder's reductions (dgl/model/models.py:147-149), run after the two
@@ -299,13 +309,14 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * matrix-core backward for complete graphs of 9..16 nodes too; those of <= 8 always run the VALU one), "bwd_mfma_cpw" (channel blocks per wave of the matrix-core
  * backward, 1 or 2), "bwd_pre2", "fwd_regular_split" (0, default: whole planes); compress GEMM
  * kernel variants "gemm_nn" / "gemm_nt" (-1, default: the per-shape choice; 0..5: compress_gemm.hip's
- * variant table). */
+ * variant table); "edge_gemm" (1, default: mrp_edge_logits_fwd on 32x32x2 MFMAs; 0: 16x16x4). */
 int mrp_tuning_set(const char* name, int32_t value);
 
-/* Library identification: ABI version (incremented on signature changes; 12 = this header: the
- * aggregation and epilogue entry points of v10 plus the matrix-core compress forward and gradients,
- * mrp_compress_fwd / _bwd_data / _bwd_weight (v11's forward-only fused and two-source compress
- * kernels, their weight packing and mrp_film_gate are gone)). */
+/* Library identification: ABI version (incremented on signature changes; 13 = this header: the
+ * aggregation and epilogue entry points of v10, the matrix-core compress forward and gradients,
+ * mrp_compress_fwd / _bwd_data / _bwd_weight of v12 (v11's forward-only fused and two-source
+ * compress kernels, their weight packing and mrp_film_gate are gone), and the edge encoder's
+ * second Linear, mrp_edge_logits_fwd). */
 int mrp_abi_version(void);
 
 /* Human-readable text for a return code (static storage). */

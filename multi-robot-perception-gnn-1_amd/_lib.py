@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "mrp_compress_bwd_weight_workspace",
     "mrp_compress_bwd_weight",
     "mrp_edge_hidden_fwd",
+    "mrp_edge_logits_fwd",
     "mrp_edge_encoder_bwd_workspace",
     "mrp_edge_encoder_bwd",
     "mrp_frame_graph_build",
@@ -38,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 12
+ABI_VERSION = 13
 MAX_NODES = 16
 
 HIP_ERROR_NOT_SUPPORTED = 801  # hipErrorNotSupported: a fused path declines this shape
@@ -105,6 +106,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_compress_bwd_weight.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
+    lib.mrp_edge_logits_fwd.argtypes = [_P, _I32, _I32, _P, _P, _P, _P]
+    lib.mrp_edge_logits_fwd.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]
     lib.mrp_edge_encoder_bwd_workspace.restype = ctypes.c_int64
     lib.mrp_edge_encoder_bwd.argtypes = [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P]

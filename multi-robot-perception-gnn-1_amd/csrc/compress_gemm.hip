@@ -48,10 +48,11 @@ namespace mrp_cg {
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-template <int MF_, int BK_, int NBUF_, int WM_, int WN_>
+template <int MF_, int BK_, int NBUF_, int WM_, int WN_, int WT_ = 64>
 struct Cfg {
   static constexpr int MF = MF_, BK = BK_, NBUF = NBUF_, WM = WM_, WN = WN_;
-  static constexpr int TM = 64 * WM, TN = 64 * WN;
+  static constexpr int WT = WT_;  // wave tile WT x WT (64, or 32 for small products)
+  static constexpr int TM = WT * WM, TN = WT * WN;
   static constexpr int NW = WM * WN, THREADS = 64 * NW;
   static constexpr int A_FLOATS = TM * BK, B_FLOATS = BK * TN, BUF = A_FLOATS + B_FLOATS;
   static constexpr int LDS = NBUF * BUF * 4;
@@ -62,7 +63,7 @@ struct Cfg {
   static constexpr int RPP = 64 / CPR;                                         // A-image rows per piece
   static constexpr int CPRB = TN / 4;                                          // chunks per NN-B row
   static constexpr int RPPB = 64 / CPRB;                                       // NN-B rows per piece
-  static constexpr int FB = 64 / MF;                                           // fragment blocks per wave side
+  static constexpr int FB = WT / MF;                                           // fragment blocks per wave side
   static constexpr int T = MF == 16 ? 4 : 8;                                   // k-steps per 16-k group
   static constexpr int CH = MF == 16 ? 1 : 2;                                  // 16-B A reads per group
   static_assert(A_PIECES % NW == 0 && B_PIECES % NW == 0, "pieces must divide over the waves");
@@ -325,8 +326,8 @@ __global__ void __launch_bounds__(G::THREADS, G::WG_PER_CU) gemm_nn(NNArgs a) {
 
   const int wm = w / G::WN, wn = w % G::WN;
   int aoff[G::BK / 16][G::CH], boff[G::FB][G::CH];
-  a_offsets<G>(wm * 64, lane, aoff);
-  bnn_offsets<G>(wn * 64, lane, boff);
+  a_offsets<G>(wm * G::WT, lane, aoff);
+  bnn_offsets<G>(wn * G::WT, lane, boff);
   typename AC::T acc[G::FB][G::FB];
 #pragma unroll
   for (int mb = 0; mb < G::FB; ++mb)
@@ -350,7 +351,7 @@ __global__ void __launch_bounds__(G::THREADS, G::WG_PER_CU) gemm_nn(NNArgs a) {
   // ---- epilogue: accumulator (row, col) of each block, + bias, to the row's destination
 #pragma unroll
   for (int nb = 0; nb < G::FB; ++nb) {
-    const int64_t col = nbase + wn * 64 + nb * G::MF + AC::col(lane);
+    const int64_t col = nbase + wn * G::WT + nb * G::MF + AC::col(lane);
     if (col >= a.ncols) continue;
     const int64_t node = col / a.P;
     const int64_t p = col - node * a.P;
@@ -358,7 +359,7 @@ __global__ void __launch_bounds__(G::THREADS, G::WG_PER_CU) gemm_nn(NNArgs a) {
     for (int mb = 0; mb < G::FB; ++mb) {
 #pragma unroll
       for (int r = 0; r < AC::R; ++r) {
-        const int row = mbase + wm * 64 + mb * G::MF + AC::row(lane, r);
+        const int row = mbase + wm * G::WT + mb * G::MF + AC::row(lane, r);
         if (row >= a.M) continue;
         float v = acc[mb][nb][r];
         if (a.bias != nullptr) v = __fadd_rn(v, a.bias[row]);
@@ -385,6 +386,7 @@ struct NTArgs {
   int64_t s1s;
   float* out;      // [split][M][N]
   float* outb;     // [split][M] or null
+  const float* colbias;  // (N) added to out (one split only), or null
   int64_t ktot;    // nodes * P
   int64_t kchunk;  // k per split, a multiple of BK
   int32_t M, N, n0, P, mtiles, ntiles;
@@ -452,8 +454,8 @@ __global__ void __launch_bounds__(G::THREADS, G::WG_PER_CU) gemm_nt(NTArgs a) {
   const int wm = w / G::WN, wn = w % G::WN;
   const bool do_db = a.outb != nullptr && nt == 0 && wn == 0;  // wave-uniform
   int aoff[G::BK / 16][G::CH], boff[G::BK / 16][G::CH];
-  a_offsets<G>(wm * 64, lane, aoff);
-  a_offsets<G>(wn * 64, lane, boff);
+  a_offsets<G>(wm * G::WT, lane, aoff);
+  a_offsets<G>(wn * G::WT, lane, boff);
   typename AC::T acc[G::FB][G::FB];
   float dbs[G::FB];
 #pragma unroll
@@ -491,14 +493,14 @@ __global__ void __launch_bounds__(G::THREADS, G::WG_PER_CU) gemm_nt(NTArgs a) {
   float* out = a.out + (int64_t)split * a.M * a.N;
 #pragma unroll
   for (int nb = 0; nb < G::FB; ++nb) {
-    const int col = nbase + wn * 64 + nb * G::MF + AC::col(lane);
+    const int col = nbase + wn * G::WT + nb * G::MF + AC::col(lane);
     if (col >= a.N) continue;
 #pragma unroll
     for (int mb = 0; mb < G::FB; ++mb)
 #pragma unroll
       for (int r = 0; r < AC::R; ++r) {
-        const int row = mbase + wm * 64 + mb * G::MF + AC::row(lane, r);
-        if (row < a.M) out[(int64_t)row * a.N + col] = acc[mb][nb][r];
+        const int row = mbase + wm * G::WT + mb * G::MF + AC::row(lane, r);
+        if (row < a.M) out[(int64_t)row * a.N + col] = a.colbias ? __fadd_rn(acc[mb][nb][r], a.colbias[col]) : acc[mb][nb][r];
       }
   }
   if (do_db) {
@@ -508,7 +510,7 @@ __global__ void __launch_bounds__(G::THREADS, G::WG_PER_CU) gemm_nt(NTArgs a) {
       float v = dbs[mb];
       if (G::MF == 16) v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
-      const int row = mbase + wm * 64 + mb * G::MF + AC::col(lane);
+      const int row = mbase + wm * G::WT + mb * G::MF + AC::col(lane);
       if ((G::MF == 16 ? (lane >> 4) : (lane >> 5)) == 0 && row < a.M) a.outb[(int64_t)split * a.M + row] = v;
     }
   }
@@ -787,7 +789,7 @@ extern "C" int mrp_compress_bwd_weight(const float* gy, int64_t gy_node_stride, 
   const int64_t need = sp.nsplit == 1 ? 0 : ((int64_t)sp.nsplit * M * N + (int64_t)sp.nsplit * M) * 4;
   if (need > 0 && (workspace == nullptr || workspace_bytes < need || !aligned16(workspace))) return hipErrorInvalidValue;
   float* ws = static_cast<float*>(workspace);
-  NTArgs a;
+  NTArgs a = {};
   a.g = gy;
   a.gs = gy_node_stride;
   a.s0 = x;
@@ -809,4 +811,43 @@ extern "C" int mrp_compress_bwd_weight(const float* gy, int64_t gy_node_stride, 
   hipLaunchKernelGGL(split_sum, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<const f4*>(ws), sp.nsplit, n4,
                      reinterpret_cast<f4*>(gw), a.outb, (int32_t)M, gbias);
   return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Edge encoder, second Linear (dgl/model/models.py:146-149): z = h W2^T + b2 for h (E, C), W2 (2C, C)
+// (nn.Linear weight layout), b2 (2C) -> z (E, 2C).  Both operands are K-contiguous (the NT product of
+// the weight gradient with one "node" of P = C pixels): 64 x 64 workgroup tiles of four 32 x 32
+// waves give E/64 x 2C/64 workgroups (448 at the headline: 1792 edges, C = 512) with the whole
+// K = C per workgroup — no split, no partial sums; the bias is added in the epilogue.
+// ------------------------------------------------------------------------------------------------
+namespace mrp_cg {
+using VE0 = Cfg<16, 32, 2, 2, 2, 32>;
+using VE1 = Cfg<32, 32, 2, 2, 2, 32>;
+}  // namespace mrp_cg
+
+extern "C" int mrp_edge_logits_fwd(const float* h, int32_t num_edges, int32_t C, const float* w2, const float* b2,
+                                   float* z, void* stream) {
+  if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
+  if (num_edges == 0 || C == 0) return hipSuccess;
+  if (!h || !w2 || !z) return hipErrorInvalidValue;
+  if (C % VE1::BK != 0 || !aligned16(h) || !aligned16(w2)) return hipErrorNotSupported;
+  if ((int64_t)num_edges * C * 4 >= kOffMax || (int64_t)2 * C * C * 4 >= kOffMax) return hipErrorNotSupported;
+  NTArgs a = {};
+  a.g = h;
+  a.gs = (int64_t)num_edges * C;  // one "node": rows m = edges, k = the C hidden units
+  a.s0 = w2;
+  a.s0s = (int64_t)2 * C * C;
+  a.s1 = w2;
+  a.s1s = a.s0s;
+  a.out = z;
+  a.outb = nullptr;
+  a.colbias = b2;
+  a.ktot = C;
+  a.kchunk = C;
+  a.M = num_edges;
+  a.N = 2 * C;
+  a.n0 = 2 * C;  // every B row from w2
+  a.P = C;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  return mrp_host::tuning().edge_gemm == 0 ? launch_nt_cfg<VE0>(a, 1, st) : launch_nt_cfg<VE1>(a, 1, st);
 }

@@ -72,7 +72,7 @@ Tuning& tuning() {
 
 extern "C" {
 
-int mrp_abi_version(void) { return 12; }
+int mrp_abi_version(void) { return 13; }
 
 int mrp_tuning_set(const char* name, int32_t value) {
   if (name == nullptr) return hipErrorInvalidValue;
@@ -105,6 +105,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"bwd_mfma_cpw", &t.bwd_mfma_cpw, 1, 2},
       {"gemm_nn", &t.gemm_nn, -1, 5},
       {"gemm_nt", &t.gemm_nt, -1, 5},
+      {"edge_gemm", &t.edge_gemm, 0, 1},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {

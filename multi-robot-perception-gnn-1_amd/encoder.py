@@ -3,8 +3,9 @@
 ``z = W2 relu(W1 pose + b1) + b2``, ``gamma/beta = sigmoid(z)``:
 
 * ``relu(W1 pose + b1)`` — one HIP kernel (``mrp_edge_hidden_fwd``; K = 9, a streaming write);
-* ``h W2^T + b2``        — a plain library GEMM (``torch.addmm`` -> hipBLASLt/rocBLAS, bias in the
-  epilogue): the encoder's only dense contraction;
+* ``h W2^T + b2``        — the encoder's only dense contraction, on the matrix cores
+  (``mrp_edge_logits_fwd``: 64 x 64 tiles, whole K per workgroup, bias in the epilogue; C % 32 != 0
+  or ``set_logits_path("library")`` runs ``torch.addmm`` -> hipBLASLt instead);
 * ``sigmoid``            — not run here: the aggregation kernels take the logits
   (``MRP_AGG_GB_LOGITS``) and apply it while building their tiles.
 
@@ -42,6 +43,36 @@ def hidden_forward(pose, w1, b1) -> torch.Tensor:
                                        ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream))
     _lib.check(code, "mrp_edge_hidden_fwd")
     return h
+
+
+_LOGITS_PATH = "hip"
+
+
+def set_logits_path(path: str) -> None:
+    """"hip" (default): ``mrp_edge_logits_fwd``; "library": ``torch.addmm`` (comparison runs)."""
+    global _LOGITS_PATH
+    if path not in ("hip", "library"):
+        raise ValueError(f"unknown logits path {path!r}")
+    _LOGITS_PATH = path
+
+
+def logits_forward(h, w2, b2) -> torch.Tensor:
+    """z = h @ w2.T + b2, (E, 2C)."""
+    E, C = h.shape
+    if tuple(w2.shape) != (2 * C, C) or tuple(b2.shape) != (2 * C,):
+        raise ValueError("edge logits shapes must be h (E,C), w2 (2C,C), b2 (2C,)")
+    if not h.is_cuda:
+        raise RuntimeError("mrp_gnn: the edge logits kernel runs only on the GPU; no CPU fallback")
+    h, w2, b2 = (t.contiguous().float() for t in (h, w2, b2))
+    if _LOGITS_PATH == "library" or C % 32 != 0:
+        return torch.addmm(b2, h, w2.t())
+    z = torch.empty((E, 2 * C), device=h.device, dtype=torch.float32)
+    lib = _lib.load_library()
+    with torch.cuda.device(h.device):
+        code = lib.mrp_edge_logits_fwd(_ptr(h), E, C, _ptr(w2), _ptr(b2), _ptr(z),
+                                       ctypes.c_void_p(torch.cuda.current_stream(h.device).cuda_stream))
+    _lib.check(code, "mrp_edge_logits_fwd")
+    return z
 
 
 class EdgeHiddenFunction(torch.autograd.Function):
@@ -94,7 +125,7 @@ class EdgeEncoderFunction(torch.autograd.Function):
     def forward(ctx, pose, w1, b1, w2, b2):
         pose = pose.contiguous().float()
         h = hidden_forward(pose, w1, b1)
-        z = torch.addmm(b2, h, w2.t())
+        z = logits_forward(h, w2, b2)
         ctx.save_for_backward(pose, w1, w2, h)
         return z
 

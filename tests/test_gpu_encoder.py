@@ -1,5 +1,7 @@
-"""GPU: the edge encoder path (HIP hidden layer + library GEMM + sigmoid fused into the
+"""GPU: the edge encoder path (HIP hidden layer + matrix-core logits GEMM + sigmoid fused into the
 aggregation) against the reference's torch layers and the golden fixtures."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -77,3 +79,37 @@ def test_logits_fusion_equals_explicit_sigmoid(cuda_device, complete, n):
     a.backward(G)
     b.backward(G)
     assert rel_err(z1.grad.cpu().numpy(), z2.grad.cpu().numpy()) <= 1e-5
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("E,C", [(1, 32), (63, 64), (65, 96), (1792, 512), (300, 1024), (129, 1280)])
+def test_logits_kernel_vs_float64(cuda_device, variant, E, C):
+    """mrp_edge_logits_fwd (both MFMA shapes) against torch fp32 and the float64 yardstick: ragged
+    edge counts (partial 64-row tiles), C % 32 == 0 from one k-stage to 40."""
+    torch.manual_seed(E * 7 + C)
+    h = torch.relu(torch.randn(E, C, device=cuda_device))
+    w2 = torch.randn(2 * C, C, device=cuda_device) / C ** 0.5
+    b2 = torch.randn(2 * C, device=cuda_device)
+    lib = m.load_library()
+    assert lib.mrp_tuning_set(b"edge_gemm", variant) == 0
+    try:
+        z = m.encoder.logits_forward(h, w2, b2)
+    finally:
+        lib.mrp_tuning_set(b"reset", 0)
+    ref = torch.addmm(b2, h, w2.t())
+    z64 = torch.addmm(b2.double(), h.double(), w2.double().t())
+    ok, errs = stack_ref.within(z, ref, z64)
+    assert ok, errs
+
+
+def test_logits_kernel_declines_unsupported_shapes(cuda_device):
+    """C % 32 != 0: the ABI says NotSupported (and logits_forward takes the library GEMM instead)."""
+    h = torch.randn(10, 48, device=cuda_device)
+    w2 = torch.randn(96, 48, device=cuda_device)
+    b2 = torch.randn(96, device=cuda_device)
+    z = torch.empty(10, 96, device=cuda_device)
+    lib = m.load_library()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    code = lib.mrp_edge_logits_fwd(p(h), 10, 48, p(w2), p(b2), p(z), ctypes.c_void_p(0))
+    assert code == m._lib.HIP_ERROR_NOT_SUPPORTED
+    assert torch.allclose(m.encoder.logits_forward(h, w2, b2), torch.addmm(b2, h, w2.t()), rtol=1e-5, atol=1e-5)
