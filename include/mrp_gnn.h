@@ -266,6 +266,17 @@ int mrp_edge_logits_fwd(const float* h, int32_t num_edges, int32_t C, const floa
                         float* z, void* stream);
 
 /*
+ * The edge encoder before its Sigmoid in one launch (dgl/model/models.py:146-149), for inference:
+ *   z = relu(pose W1^T + b1) W2^T + b2     pose (num_edges, 9), w1 (C, 9), b1 (C), w2 (2C, C), b2 (2C)
+ * The hidden layer is evaluated inside the GEMM's A tiles (bit-identical to mrp_edge_hidden_fwd) and
+ * never written; training keeps h for its backward and runs mrp_edge_hidden_fwd + mrp_edge_logits_fwd.
+ * Requirements (else hipErrorNotSupported): C % 32 == 0, w1, b1, w2 16-byte aligned, W1 and b1 plus
+ * the stage buffers within 160 KiB of LDS (C <= 2816).
+ */
+int mrp_edge_encoder_fwd(const float* pose, const float* w1, const float* b1, const float* w2,
+                         const float* b2, int32_t num_edges, int32_t C, float* z, void* stream);
+
+/*
  * Backward of the edge encoder's reductions (dgl/model/models.py:147-149), run after the two
  * library GEMMs of its backward (dh = dz W2, dW2 = dz^T h):
  *   db2[j]    = sum_e dz[e, j]                              (dz: (E, 2C), the logits' gradient that
@@ -309,14 +320,15 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * matrix-core backward for complete graphs of 9..16 nodes too; those of <= 8 always run the VALU one), "bwd_mfma_cpw" (channel blocks per wave of the matrix-core
  * backward, 1 or 2), "bwd_pre2", "fwd_regular_split" (0, default: whole planes); compress GEMM
  * kernel variants "gemm_nn" / "gemm_nt" (-1, default: the per-shape choice; 0..5: compress_gemm.hip's
- * variant table); "edge_gemm" (1, default: mrp_edge_logits_fwd on 32x32x2 MFMAs; 0: 16x16x4). */
+ * variant table); "edge_gemm" (1, default: mrp_edge_logits_fwd on 32x32x2 MFMAs; 0: 16x16x4); "edge_fused"
+ * (mrp_edge_encoder_fwd tile/buffer variant, 0..4). */
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 13 = this header: the
  * aggregation and epilogue entry points of v10, the matrix-core compress forward and gradients,
  * mrp_compress_fwd / _bwd_data / _bwd_weight of v12 (v11's forward-only fused and two-source
  * compress kernels, their weight packing and mrp_film_gate are gone), and the edge encoder's
- * second Linear, mrp_edge_logits_fwd). */
+ * second Linear and whole forward, mrp_edge_logits_fwd / mrp_edge_encoder_fwd). */
 int mrp_abi_version(void);
 
 /* Human-readable text for a return code (static storage). */

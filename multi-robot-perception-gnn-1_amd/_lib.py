@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "mrp_compress_bwd_weight",
     "mrp_edge_hidden_fwd",
     "mrp_edge_logits_fwd",
+    "mrp_edge_encoder_fwd",
     "mrp_edge_encoder_bwd_workspace",
     "mrp_edge_encoder_bwd",
     "mrp_frame_graph_build",
@@ -108,6 +109,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
     lib.mrp_edge_logits_fwd.argtypes = [_P, _I32, _I32, _P, _P, _P, _P]
     lib.mrp_edge_logits_fwd.restype = ctypes.c_int
+    lib.mrp_edge_encoder_fwd.argtypes = [_P, _P, _P, _P, _P, _I32, _I32, _P, _P]
+    lib.mrp_edge_encoder_fwd.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]
     lib.mrp_edge_encoder_bwd_workspace.restype = ctypes.c_int64
     lib.mrp_edge_encoder_bwd.argtypes = [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P]

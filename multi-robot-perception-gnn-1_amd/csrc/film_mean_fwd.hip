@@ -106,6 +106,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"gemm_nn", &t.gemm_nn, -1, 5},
       {"gemm_nt", &t.gemm_nt, -1, 5},
       {"edge_gemm", &t.edge_gemm, 0, 1},
+      {"edge_fused", &t.edge_fused, 0, 4},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {

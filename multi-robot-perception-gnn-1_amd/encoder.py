@@ -9,6 +9,9 @@
 * ``sigmoid``            — not run here: the aggregation kernels take the logits
   (``MRP_AGG_GB_LOGITS``) and apply it while building their tiles.
 
+Inference (no gradient wanted) runs the first two as one kernel, ``mrp_edge_encoder_fwd``: the hidden
+layer is evaluated inside the GEMM's A tiles and never written.
+
 Backward (training): the two GEMMs of the second Linear (``dh = dz W2`` and ``dW2 = dz^T h``) run
 concurrently on two streams — each alone fills only part of the chip at E = 1792 — and every small
 reduction (the ReLU mask, ``dW1``, ``db1``, ``db2``) runs in one HIP pass (``mrp_edge_encoder_bwd``)
@@ -45,15 +48,35 @@ def hidden_forward(pose, w1, b1) -> torch.Tensor:
     return h
 
 
-_LOGITS_PATH = "hip"
+_LOGITS_PATH = "fused"
 
 
 def set_logits_path(path: str) -> None:
-    """"hip" (default): ``mrp_edge_logits_fwd``; "library": ``torch.addmm`` (comparison runs)."""
+    """"fused" (default): ``mrp_edge_encoder_fwd`` when no gradient is wanted, else as "hip";
+    "hip": ``mrp_edge_hidden_fwd`` + ``mrp_edge_logits_fwd``; "library": the hidden kernel +
+    ``torch.addmm`` (comparison runs)."""
     global _LOGITS_PATH
-    if path not in ("hip", "library"):
+    if path not in ("fused", "hip", "library"):
         raise ValueError(f"unknown logits path {path!r}")
     _LOGITS_PATH = path
+
+
+def encoder_forward_fused(pose, w1, b1, w2, b2) -> torch.Tensor:
+    """z = relu(pose W1^T + b1) W2^T + b2, (E, 2C), in one launch (``mrp_edge_encoder_fwd``); None
+    when the kernel declines the shape."""
+    E, C = pose.shape[0], w1.shape[0]
+    if not pose.is_cuda:
+        raise RuntimeError("mrp_gnn: the edge encoder kernel runs only on the GPU; no CPU fallback")
+    pose, w1, b1, w2, b2 = (t.detach().contiguous().float() for t in (pose, w1, b1, w2, b2))
+    z = torch.empty((E, 2 * C), device=pose.device, dtype=torch.float32)
+    lib = _lib.load_library()
+    with torch.cuda.device(pose.device):
+        code = lib.mrp_edge_encoder_fwd(_ptr(pose), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), E, C, _ptr(z),
+                                        ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream))
+    if code == _lib.HIP_ERROR_NOT_SUPPORTED:
+        return None
+    _lib.check(code, "mrp_edge_encoder_fwd")
+    return z
 
 
 def logits_forward(h, w2, b2) -> torch.Tensor:
@@ -161,4 +184,9 @@ def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Te
     l1, l2 = enc_layers[0], enc_layers[2]
     if not pose.is_cuda:
         raise RuntimeError("mrp_gnn: the edge encoder kernels run only on the GPU; no CPU fallback")
-    return EdgeEncoderFunction.apply(pose, l1.weight, l1.bias, l2.weight, l2.bias)
+    params = (pose, l1.weight, l1.bias, l2.weight, l2.bias)
+    if _LOGITS_PATH == "fused" and not (torch.is_grad_enabled() and any(t.requires_grad for t in params)):
+        z = encoder_forward_fused(*params)
+        if z is not None:
+            return z
+    return EdgeEncoderFunction.apply(*params)

@@ -113,3 +113,50 @@ def test_logits_kernel_declines_unsupported_shapes(cuda_device):
     code = lib.mrp_edge_logits_fwd(p(h), 10, 48, p(w2), p(b2), p(z), ctypes.c_void_p(0))
     assert code == m._lib.HIP_ERROR_NOT_SUPPORTED
     assert torch.allclose(m.encoder.logits_forward(h, w2, b2), torch.addmm(b2, h, w2.t()), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("E,C", [(1, 32), (65, 64), (1792, 512), (200, 1024), (129, 2048)])
+def test_fused_encoder_equals_two_kernel_path(cuda_device, variant, E, C):
+    """mrp_edge_encoder_fwd (every tile/buffer variant) gives exactly the two-kernel result (the
+    hidden layer's arithmetic is the same, and so is each output's MFMA k order), and is within
+    the float64 yardstick of the reference layers."""
+    torch.manual_seed(E + C + variant)
+    enc = m.edge_encoder([C, C]).to(cuda_device)
+    pose = (torch.randn(E, 9) * 5).to(cuda_device)
+    l1, l2 = enc.layers[0], enc.layers[2]
+    lib = m.load_library()
+    assert lib.mrp_tuning_set(b"edge_fused", variant) == 0
+    try:
+        with torch.no_grad():
+            z = m.encoder.encoder_forward_fused(pose, l1.weight, l1.bias, l2.weight, l2.bias)
+            ref = m.encoder.logits_forward(m.encoder.hidden_forward(pose, l1.weight, l1.bias), l2.weight, l2.bias)
+    finally:
+        lib.mrp_tuning_set(b"reset", 0)
+    wn, nbuf = ((2, 2), (2, 3), (4, 2), (4, 3), (4, 4))[variant]  # compress_gemm.hip MRP_ENC_VARIANTS
+    lds = nbuf * (64 * 32 + 32 * wn * 32) * 4 + C * 10 * 4
+    if lds > 160 * 1024:
+        assert z is None  # declined: stage buffers + W1 exceed the LDS
+        return
+    assert z is not None and torch.equal(z, ref)
+    with torch.no_grad():
+        t32 = l2(torch.relu(l1(pose)))
+        p64 = [t.detach().double() for t in enc.parameters()]
+        z64 = torch.nn.functional.linear(torch.relu(torch.nn.functional.linear(pose.double(), p64[0], p64[1])),
+                                         p64[2], p64[3])
+    ok, errs = stack_ref.within(z, t32, z64)
+    assert ok, errs
+
+
+def test_edge_logits_takes_fused_kernel_only_without_grad(cuda_device):
+    """edge_logits: inference -> the fused kernel; with gradients wanted -> the two-kernel autograd
+    path; a shape the fused kernel declines (C % 32) -> the two-kernel path (same values)."""
+    torch.manual_seed(0)
+    for C in (64, 48):
+        enc = m.edge_encoder([C, C]).to(cuda_device)
+        pose = torch.randn(100, 9, device=cuda_device)
+        with torch.no_grad():
+            z0 = m.encoder.edge_logits(enc.layers, pose)
+        z1 = m.encoder.edge_logits(enc.layers, pose)
+        assert z1.requires_grad and not z0.requires_grad
+        assert torch.allclose(z0, z1.detach(), rtol=1e-6, atol=1e-6)

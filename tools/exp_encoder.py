@@ -1,6 +1,7 @@
 """Kernel lab (not product code): the edge encoder's second Linear z = h W2^T + b2 — the matrix-core
 kernel mrp_edge_logits_fwd (mrp_tuning_set "edge_gemm" 0 / 1) against torch.addmm (hipBLASLt) —
-and the whole encoder forward (hidden kernel + logits), HIP-graph timed (bench.time_launches), at
+the one-launch encoder mrp_edge_encoder_fwd ("edge_fused" 0..4), and the whole encoder forward per
+path (library / hidden + logits kernels / fused), HIP-graph timed (bench.time_launches), at
 the headline size (B = 32 complete graphs of 8: E = 1792, C = 512) and the BASELINE configs.
 
 usage: python tools/exp_encoder.py [--iters N]"""
@@ -44,7 +45,20 @@ for name, E, C in SHAPES:
             t = time_launches([lambda: enc.logits_forward(h, w2, b2)], args.iters, dev)
             row.append(f"v{v} {t * 1e6:6.1f} us {flop / t / 1e12:5.1f} TF/s (err {err:.1e})")
         lib.mrp_tuning_set(b"reset", 0)
-        for path in ("library", "hip"):
+        l1 = layers[0]
+        ref_full = enc.logits_forward(enc.hidden_forward(pose, l1.weight, l1.bias), w2, b2)
+        for v in range(5):
+            lib.mrp_tuning_set(b"edge_fused", v)
+            args_f = (pose, l1.weight, l1.bias, w2, b2)
+            z = enc.encoder_forward_fused(*args_f)
+            if z is None:
+                row.append(f"fused{v} declined")
+                continue
+            same = bool(torch.equal(z, ref_full))
+            t = time_launches([lambda: enc.encoder_forward_fused(*args_f)], args.iters, dev)
+            row.append(f"fused{v} {t * 1e6:6.1f} us{'' if same else ' MISMATCH'}")
+        lib.mrp_tuning_set(b"reset", 0)
+        for path in ("library", "hip", "fused"):
             enc.set_logits_path(path)
             t = time_launches([lambda: enc.edge_logits(layers, pose)], args.iters, dev)
             row.append(f"encoder[{path}] {t * 1e6:6.1f} us")

@@ -13,9 +13,26 @@ from mrp_gnn_amd import compress as cp  # noqa: E402
 SHAPES = {"cfg1": (128, 512, 32), "cfg2": (256, 1280, 8), "cfg3": (64, 2048, 8), "cfg4": (128, 1024, 16)}
 name = sys.argv[1] if len(sys.argv) > 1 else "cfg3"
 variant = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-n, C, H = SHAPES[name]
 dev = torch.device("cuda:0")
 lib = mrp.load_library()
+if name == "enc":  # the headline's edge encoder: fused kernel (edge_fused = variant) and addmm
+    from mrp_gnn_amd import encoder as enc
+    E, C = 1792, 512
+    layers = mrp.edge_encoder([C, C]).to(dev).layers
+    pose = torch.randn(E, 9, device=dev)
+    h = torch.relu(torch.randn(E, C, device=dev))
+    p = [t.detach() for t in (pose, layers[0].weight, layers[0].bias, layers[2].weight, layers[2].bias)]
+    lib.mrp_tuning_set(b"edge_fused", variant)
+    for _ in range(30):
+        enc.encoder_forward_fused(*p)
+    torch.cuda.synchronize()
+    for _ in range(5):
+        enc.encoder_forward_fused(*p)
+        torch.addmm(p[4], h, p[3].t())
+    torch.cuda.synchronize()
+    print("done")
+    sys.exit(0)
+n, C, H = SHAPES[name]
 lib.mrp_tuning_set(b"gemm_nn", variant)
 x = torch.randn(n, C, H, H, device=dev)
 a = torch.randn_like(x)
