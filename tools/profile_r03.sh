@@ -2,10 +2,10 @@
 # Profile the aggregation kernels at every BASELINE config shape (tools/prof_kernels.py) and the
 # headline bench command on the GPU box: kernel trace + stats, then one PMC pass per counter group
 # (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950; <= 8 SQ counters per pass).
-# Usage: tools/profile_r02.sh <round> ; output under gpurun_out/prof_<round>/, summarised into
+# Usage: tools/profile_r03.sh <round> ; output under gpurun_out/prof_<round>/, summarised into
 # profiles/ by tools/pmc_summary.py.
 set -euo pipefail
-R=${1:-r02}
+R=${1:-r03}
 ITERS=${ITERS:-20}
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd /tmp && export TMPDIR=/tmp
@@ -17,6 +17,8 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/bench" -o run --outp
   -- python3 bench.py $BENCH_ARGS > "$OUT/bench_trace.log" 2>&1
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
   -- python3 tools/prof_kernels.py "$ITERS" > "$OUT/trace.log" 2>&1
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/train" -o run --output-format csv \
+  -- python3 tools/prof_train_step.py 5 > "$OUT/train.log" 2>&1
 pass() {  # name counters...
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" --kernel-include-regex "film_" -d "$OUT/pmc_$name" -o run \
