@@ -277,6 +277,24 @@ int mrp_edge_encoder_fwd(const float* pose, const float* w1, const float* b1, co
                          const float* b2, int32_t num_edges, int32_t C, float* z, void* stream);
 
 /*
+ * The same forward at fp32 accuracy on the bf16 matrix cores (encoder_split.hip): every fp32 operand is
+ * split exactly into three bf16 parts and each product is the sum of the six partial products whose
+ * omitted terms are below 2^-25 of it (error against float64 at or below an fp32 GEMM's); the hidden
+ * layer is computed on the matrix cores too (b1 as a tenth input of value 1.0) and never written.
+ * The weights are split and laid out once per weight version:
+ *   mrp_edge_encoder_pack_bytes(C)  bytes of the packed image (0 if C <= 0 or C % 32 != 0)
+ *   mrp_edge_encoder_pack           w1 (C, 9), b1 (C), w2 (2C, C) -> packed (16-byte aligned device buffer)
+ *   mrp_edge_encoder_fwd_split      z = relu(pose W1^T + b1) W2^T + b2 from pose (E, 9), the packed image
+ *                                   and b2 (2C, or NULL) -> z (E, 2C)
+ * Requirements (else hipErrorNotSupported): C % 32 == 0.  Used for inference; training keeps h for its
+ * backward and runs mrp_edge_hidden_fwd + mrp_edge_logits_fwd.
+ */
+int64_t mrp_edge_encoder_pack_bytes(int32_t C);
+int mrp_edge_encoder_pack(const float* w1, const float* b1, const float* w2, int32_t C, void* packed, void* stream);
+int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const float* b2, int32_t num_edges, int32_t C,
+                               float* z, void* stream);
+
+/*
  * Backward of the edge encoder's reductions (dgl/model/models.py:147-149), run after the two
  * library GEMMs of its backward (dh = dz W2, dW2 = dz^T h):
  *   db2[j]    = sum_e dz[e, j]                              (dz: (E, 2C), the logits' gradient that
@@ -324,7 +342,9 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * (mrp_edge_encoder_fwd tile/buffer variant, 0..4). */
 int mrp_tuning_set(const char* name, int32_t value);
 
-/* Library identification: ABI version (incremented on signature changes; 13 = this header: the
+/* Library identification: ABI version (incremented on signature changes; 14 = this header: v13 plus
+ * the split-bf16 edge encoder forward and its weight packing (mrp_edge_encoder_pack_bytes /
+ * _pack / _fwd_split); 13: the
  * aggregation and epilogue entry points of v10, the matrix-core compress forward and gradients,
  * mrp_compress_fwd / _bwd_data / _bwd_weight of v12 (v11's forward-only fused and two-source
  * compress kernels, their weight packing and mrp_film_gate are gone), and the edge encoder's

@@ -33,6 +33,9 @@ EXPORTED_SYMBOLS = (
     "mrp_edge_hidden_fwd",
     "mrp_edge_logits_fwd",
     "mrp_edge_encoder_fwd",
+    "mrp_edge_encoder_pack_bytes",
+    "mrp_edge_encoder_pack",
+    "mrp_edge_encoder_fwd_split",
     "mrp_edge_encoder_bwd_workspace",
     "mrp_edge_encoder_bwd",
     "mrp_frame_graph_build",
@@ -40,7 +43,7 @@ EXPORTED_SYMBOLS = (
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 13
+ABI_VERSION = 14
 MAX_NODES = 16
 
 HIP_ERROR_NOT_SUPPORTED = 801  # hipErrorNotSupported: a fused path declines this shape
@@ -111,6 +114,12 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_edge_logits_fwd.restype = ctypes.c_int
     lib.mrp_edge_encoder_fwd.argtypes = [_P, _P, _P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_encoder_fwd.restype = ctypes.c_int
+    lib.mrp_edge_encoder_pack_bytes.argtypes = [_I32]
+    lib.mrp_edge_encoder_pack_bytes.restype = ctypes.c_int64
+    lib.mrp_edge_encoder_pack.argtypes = [_P, _P, _P, _I32, _P, _P]
+    lib.mrp_edge_encoder_pack.restype = ctypes.c_int
+    lib.mrp_edge_encoder_fwd_split.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
+    lib.mrp_edge_encoder_fwd_split.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]
     lib.mrp_edge_encoder_bwd_workspace.restype = ctypes.c_int64
     lib.mrp_edge_encoder_bwd.argtypes = [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P]

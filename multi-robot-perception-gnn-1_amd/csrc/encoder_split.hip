@@ -1,0 +1,361 @@
+// encoder_split.hip — the edge encoder before its Sigmoid in one launch on the bf16 matrix cores,
+// at fp32 accuracy, gfx950 (MI355X / CDNA4).
+//
+// Reference (xjh19971/multi-robot-perception-gnn-1, dgl/model/models.py:146-149):
+//     z = Linear(C, 2C)(ReLU(Linear(9, C)(pose)))          pose (E, 9) -> z (E, 2C)
+// (the Sigmoid of models.py:150 runs inside the aggregation kernels, MRP_AGG_GB_LOGITS).
+//
+// Arithmetic.  Every fp32 operand value x is split exactly into three bf16 parts,
+//     x = x0 + x1 + x2 (+ a residual below 2^-24 |x|),  x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)
+// (each subtraction is exact in fp32; round-to-nearest conversions, v_cvt_pk_bf16_f32), and a product
+// a b is the sum of the six partial products a_i b_j with i + j <= 2 — each exact in the MFMA (8 x 8
+// significant bits), summed into an fp32 accumulator, smallest terms first.  The omitted terms are
+// below 2^-25 |a b|, so the result is as accurate as an fp32 GEMM (tests/test_gpu_encoder.py checks
+// it against float64 with the same yardstick as the fp32 kernels); it runs on
+// v_mfma_f32_32x32x16_bf16, six of which cost 192 cycles per 16 k against 512 for the fp32 MFMA.
+//
+// Structure.  One wave owns 32 edges x 64 output columns; the four waves of a workgroup share a
+// column slab, whose weight fragments arrive once per workgroup by LDS-DMA (four stages, two ahead).
+// Per block of 32 hidden units a wave
+//   1. computes X = W1' pose'^T (32 units x 32 edges) on the MFMAs: k = the 9 pose values, then 1.0
+//      against b1 (so the bias is one more product), zero-padded to 16;
+//   2. applies the ReLU and splits X into bf16 parts in registers — X's accumulator layout (edge on
+//      the lane, units in the registers) IS the A operand of z = X^T W2^T (a sum over X's row index:
+//      cdna_hip_programming.md §3, accumulator as operand) with a permuted k order inside each 16-k
+//      step, which the packed W2 image reproduces;
+//   3. accumulates z for its 64 columns (two 32 x 32 blocks).
+// The weights are split and laid out once per weight version by mrp_edge_encoder_pack, in the exact
+// per-lane fragment order, so every weight load of a wave is one contiguous KiB.
+// Work per launch at the headline (E = 1792, C = 512): 224 workgroups of four waves; h is computed
+// once per (32 edges, 64 columns) wave: 6 MFMAs per hidden block against 24 for z.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mrp_gnn.h"
+
+namespace mrp_x6 {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+
+constexpr int kNin = 9;
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+
+// two fp32 -> two bf16 (round to nearest even) in one dword: v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t cvt2(f2 x) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(x, bf2)); }
+// ... and back to fp32 (exact)
+__device__ __forceinline__ f2 widen2(uint32_t p) {
+  f2 r;
+  r.x = __uint_as_float(p << 16);
+  r.y = __uint_as_float(p & 0xffff0000u);
+  return r;
+}
+
+// The three bf16 parts of 8 fp32 values (exact split, see above), pairwise: one v_cvt_pk_bf16_f32 and
+// one v_pk_add_f32 per pair and part, element j of a part in half j & 1 of dword j >> 1 (the MFMA's
+// operand order).
+__device__ __forceinline__ void split8(const float (&v)[8], bf8 (&p)[3]) {
+  u4 a, b, c;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f2 x;
+    x.x = v[2 * i];
+    x.y = v[2 * i + 1];
+    a[i] = cvt2(x);
+    const f2 r1 = x - widen2(a[i]);
+    b[i] = cvt2(r1);
+    const f2 r2 = r1 - widen2(b[i]);
+    c[i] = cvt2(r2);
+  }
+  p[0] = __builtin_bit_cast(bf8, a);
+  p[1] = __builtin_bit_cast(bf8, b);
+  p[2] = __builtin_bit_cast(bf8, c);
+}
+
+// max(x, 0) on the bit pattern (negative floats, -0 included, are negative integers): one v_max_i32
+__device__ __forceinline__ float relu(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+
+__device__ __forceinline__ bf8 as_bf8(u4 v) { return __builtin_bit_cast(bf8, v); }
+__device__ __forceinline__ u4 as_u4(bf8 v) { return __builtin_bit_cast(u4, v); }
+
+// acc += a b over the split parts: the six products with i + j <= 2, smallest first
+__device__ __forceinline__ f16v mma6(const bf8 (&a)[3], const bf8 (&b)[3], f16v acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
+// Packed image, in 16-byte units (8 bf16 = one lane's fragment of one part):
+//   W1 block hb, part p, lane l:        (hb * 3 + p) * 64 + l
+//       unit u = 32 hb + (l & 31), k = 8 (l >> 5) + j: W1[u][k] (k < 9), b1[u] (k = 9), 0 (k > 9)
+//   W2 column block cb, hidden block hb, 16-k step s, part p, lane l:
+//       w2_base + (((cb * HB + hb) * 2 + s) * 3 + p) * 64 + l
+//       column 32 cb + (l & 31), element j: hidden unit 32 hb + 16 s + 8 (j >> 2) + 4 (l >> 5) + (j & 3)
+//       — the row of X that element j of the A operand built from X's registers 8 s .. 8 s + 7 holds
+__host__ __device__ inline int64_t w1_units(int C) { return (int64_t)(C / 32) * 3 * 64; }
+__host__ __device__ inline int64_t w2_units(int C) { return (int64_t)(2 * C / 32) * (C / 32) * 2 * 3 * 64; }
+
+__global__ void __launch_bounds__(256) pack(const float* __restrict__ w1, const float* __restrict__ b1,
+                                            const float* __restrict__ w2, int C, u4* __restrict__ out) {
+  const int HB = C / 32;
+  const int64_t n1 = (int64_t)HB * 64, n2 = (int64_t)(2 * C / 32) * HB * 2 * 64;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n1 + n2) return;
+  float v[8];
+  bf8 p[3];
+  int64_t dst;
+  const int l = (int)(t & 63);
+  const int h = l >> 5;
+  if (t < n1) {
+    const int hb = (int)(t >> 6);
+    const int u = 32 * hb + (l & 31);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * h + j;
+      v[j] = k < kNin ? w1[(int64_t)u * kNin + k] : (k == kNin ? b1[u] : 0.f);
+    }
+    dst = (int64_t)hb * 3 * 64 + l;
+  } else {
+    const int64_t g = (t - n1) >> 6;  // ((cb * HB + hb) * 2 + s)
+    const int s = (int)(g & 1);
+    const int64_t cbhb = g >> 1;
+    const int hb = (int)(cbhb % HB);
+    const int cb = (int)(cbhb / HB);
+    const int col = 32 * cb + (l & 31);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = w2[(int64_t)col * C + 32 * hb + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3)];
+    dst = w1_units(C) + g * 3 * 64 + l;
+  }
+  split8(v, p);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) out[dst + q * 64] = as_u4(p[q]);
+}
+
+struct FwdArgs {
+  const float* pose;
+  const u4* packed;
+  const float* b2;
+  float* z;
+  int32_t E, C, egroups;
+};
+
+// LDS stage of one hidden block, shared by the workgroup's four waves (one per 32-edge block, one
+// column slab): 16 pieces of 1 KiB (64 lanes x 16 B, a lane's fragment at 16 lane): pieces 0..11 the
+// W2 parts of the slab's two column blocks (c, s, p) = 6 c + 3 s + p, 12..14 the W1 parts, 15 a copy
+// of 14 (so every wave issues exactly four LDS-DMA pieces per stage and counts them alike).
+constexpr int kPieces = 16, kStageU4 = kPieces * 64, kStages = 4;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+__global__ void __launch_bounds__(256) encoder_fwd(FwdArgs a) {
+  extern __shared__ u4 lds[];
+  // workgroup -> (edge group of 128, column slab of 64); consecutive ids share a slab (its W2 image)
+  // and, after the remap, an XCD and its L2
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int eg = id % a.egroups, cs = id / a.egroups;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int e0 = (eg * 4 + wv) * 32;
+  const int HB = a.C / 32;
+  const int r = lane & 31, hh = lane >> 5;
+
+  // ---- LDS-DMA: wave wv issues pieces 4 wv .. 4 wv + 3 of every stage
+  const int64_t cstride = (int64_t)HB * 2 * 3 * 64;  // 16-B units per W2 column block
+  const __amdgpu_buffer_rsrc_t rw = rsrc(a.packed);
+  uint32_t voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pc = 4 * wv + i;
+    int64_t unit;  // the piece's first unit at hidden block 0
+    if (pc < 12) {
+      const int c = pc / 6, sp = pc % 6;  // sp = 3 s + p
+      unit = w1_units(a.C) + (int64_t)(2 * cs + c) * cstride + sp * 64;
+    } else {
+      unit = (int64_t)(pc < 15 ? pc - 12 : 2) * 64;
+    }
+    voff[i] = (uint32_t)((unit + lane) * 16);
+  }
+  auto issue = [&](int hb) {
+    u4* st = lds + (hb % kStages) * kStageU4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pc = 4 * wv + i;
+      const uint32_t soff = (uint32_t)(hb * (pc < 12 ? 6 * 64 : 3 * 64) * 16);  // per hidden block
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, st + pc * 64, 16, voff[i], soff, 0, 0);
+    }
+  };
+  // pose fragment (B operand of X = W1' pose'^T): lane's edge, k = 8 hh + j; k = 9 is the 1.0 of b1
+  bf8 pp[3];
+  {
+    const int e = min(e0 + r, a.E - 1);
+    const float* pr = a.pose + (int64_t)e * kNin;
+    float v[8];
+    if (hh == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = pr[j];
+    } else {
+      v[0] = pr[8];
+      v[1] = 1.f;
+#pragma unroll
+      for (int j = 2; j < 8; ++j) v[j] = 0.f;
+    }
+    split8(v, pp);
+  }
+
+  issue(0);
+  if (HB > 1) issue(1);
+
+  f16v Z[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Z[c][i] = 0.f;
+  bf8 hp[2][3];  // the previous block's ReLU'd hidden values, split (A operand per 16-unit step)
+
+  // Stage hb landed (own pieces; the younger stage hb + 1 may still be in flight), then the barrier
+  // publishes every wave's pieces and certifies that all reads of the previous iteration are done.
+  auto stage_ready = [&](int hb) {
+    if (hb + 1 < HB)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  // a stage's fragments into registers: W1 parts first (X needs them first), then the 12 W2 parts
+  auto read_frags = [&](int hb, u4 (&w)[15]) {
+    const u4* st = lds + (hb % kStages) * kStageU4 + lane;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[12 + k] = st[(12 + k) * 64];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) w[k] = st[k * 64];
+  };
+  auto x_block = [&](const u4 (&w)[15]) {  // X = W1' pose'^T
+    bf8 wa[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) wa[p] = as_bf8(w[12 + p]);
+    f16v X;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) X[i] = 0.f;
+    return mma6(wa, pp, X);
+  };
+  auto split_x = [&](const f16v& X) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float hv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hv[j] = relu(X[8 * s + j]);
+      split8(hv, hp[s]);
+    }
+  };
+  auto z_block = [&](const u4 (&w)[15]) {  // z += relu(X)^T W2^T (hp holds relu(X) split)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        bf8 wb[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) wb[p] = as_bf8(w[6 * c + 3 * s + p]);
+        Z[c] = mma6(hp[s], wb, Z[c]);
+      }
+  };
+
+  // Iteration hb: the barrier of stage hb, DMA of stage hb + 2 into the buffer stage hb - 2 used, then
+  // stage hb's fragments into registers (in flight) while the matrix cores run X of block hb (its W1
+  // fragments are read first) and z of block hb - 1 (fragments already in registers), then X's ReLU
+  // and split on the VALU.
+  u4 F[15], G[15];
+  auto step = [&](int hb, u4 (&cur)[15], u4 (&nxt)[15]) {  // cur: stage hb - 1's fragments
+    stage_ready(hb);
+    if (hb + 2 < HB) issue(hb + 2);
+    read_frags(hb, nxt);
+    const f16v X = x_block(nxt);
+    z_block(cur);
+    split_x(X);
+  };
+  stage_ready(0);
+  if (HB > 2) issue(2);
+  read_frags(0, F);
+  split_x(x_block(F));
+  int hb = 1;
+#pragma unroll 1
+  for (; hb + 1 < HB; hb += 2) {  // two blocks per trip, so the fragment sets swap roles without copies
+    step(hb, F, G);
+    step(hb + 1, G, F);
+  }
+  if (hb < HB) {
+    step(hb, F, G);
+#pragma unroll
+    for (int k = 0; k < 15; ++k) F[k] = G[k];
+  }
+  z_block(F);
+
+  // epilogue: accumulator register i of lane (r, hh) is edge e0 + (i & 3) + 8 (i >> 2) + 4 hh, column r
+  if (e0 >= a.E) return;  // a wave past the last edge (only the stores are skipped: it took part in the barriers)
+  const int N = 2 * a.C;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int col = (2 * cs + c) * 32 + r;
+    const float bias = a.b2 != nullptr ? a.b2[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = e0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      if (e < a.E) a.z[(int64_t)e * N + col] = __fadd_rn(Z[c][i], bias);
+    }
+  }
+}
+
+}  // namespace mrp_x6
+
+using namespace mrp_x6;
+
+extern "C" int64_t mrp_edge_encoder_pack_bytes(int32_t C) {
+  if (C <= 0 || C % 32 != 0) return 0;
+  return (w1_units(C) + w2_units(C)) * 16;
+}
+
+extern "C" int mrp_edge_encoder_pack(const float* w1, const float* b1, const float* w2, int32_t C, void* packed,
+                                     void* stream) {
+  if (C <= 0) return hipErrorInvalidValue;
+  if (C % 32 != 0) return hipErrorNotSupported;
+  if (!w1 || !b1 || !w2 || !packed || (reinterpret_cast<uintptr_t>(packed) & 15)) return hipErrorInvalidValue;
+  const int64_t threads = (w1_units(C) + w2_units(C)) / 3;
+  if ((threads + 255) / 256 > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream), w1,
+                     b1, w2, C, static_cast<u4*>(packed));
+  return hipGetLastError();
+}
+
+extern "C" int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const float* b2, int32_t num_edges,
+                                          int32_t C, float* z, void* stream) {
+  if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
+  if (num_edges == 0 || C == 0) return hipSuccess;
+  if (C % 32 != 0) return hipErrorNotSupported;
+  if (!pose || !packed || !z || (reinterpret_cast<uintptr_t>(packed) & 15)) return hipErrorInvalidValue;
+  FwdArgs a;
+  a.pose = pose;
+  a.packed = static_cast<const u4*>(packed);
+  a.b2 = b2;
+  a.z = z;
+  a.E = num_edges;
+  a.C = C;
+  a.egroups = (num_edges + 127) / 128;
+  const int64_t grid = (int64_t)a.egroups * (2 * (int64_t)C / 64);
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  constexpr size_t lds = (size_t)kStages * kStageU4 * 16;  // 64 KiB
+  hipLaunchKernelGGL(encoder_fwd, dim3((unsigned)grid), dim3(256), lds, static_cast<hipStream_t>(stream), a);
+  return hipGetLastError();
+}

@@ -9,8 +9,10 @@
 * ``sigmoid``            — not run here: the aggregation kernels take the logits
   (``MRP_AGG_GB_LOGITS``) and apply it while building their tiles.
 
-Inference (no gradient wanted) runs the first two as one kernel, ``mrp_edge_encoder_fwd``: the hidden
-layer is evaluated inside the GEMM's A tiles and never written.
+Inference (no gradient wanted) runs the first two as one kernel, ``mrp_edge_encoder_fwd_split``: the
+hidden layer and the second Linear on the bf16 matrix cores at fp32 accuracy (every fp32 operand split
+exactly into three bf16 parts, six partial products; ``csrc/encoder_split.hip``), h never written.  The
+weights are split and laid out once per weight version (:func:`packed_weights`).
 
 Backward (training): the two GEMMs of the second Linear (``dh = dz W2`` and ``dW2 = dz^T h``) run
 concurrently on two streams — each alone fills only part of the chip at E = 1792 — and every small
@@ -20,6 +22,7 @@ instead of five torch launches.
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import torch
 
@@ -48,17 +51,74 @@ def hidden_forward(pose, w1, b1) -> torch.Tensor:
     return h
 
 
-_LOGITS_PATH = "fused"
+_LOGITS_PATH = "split"
 
 
 def set_logits_path(path: str) -> None:
-    """"fused" (default): ``mrp_edge_encoder_fwd`` when no gradient is wanted, else as "hip";
+    """"split" (default): ``mrp_edge_encoder_fwd_split`` (split-bf16 matrix cores) when no gradient is
+    wanted, else as "hip"; "fused": the fp32-MFMA one-launch ``mrp_edge_encoder_fwd`` likewise;
     "hip": ``mrp_edge_hidden_fwd`` + ``mrp_edge_logits_fwd``; "library": the hidden kernel +
     ``torch.addmm`` (comparison runs)."""
     global _LOGITS_PATH
-    if path not in ("fused", "hip", "library"):
+    if path not in ("split", "fused", "hip", "library"):
         raise ValueError(f"unknown logits path {path!r}")
     _LOGITS_PATH = path
+
+
+# packed split-bf16 weight images, per second-Linear module: (key, tensor).  The key holds the data
+# pointers and autograd versions of W1, b1, W2: an optimizer step (an in-place update under no_grad)
+# bumps a version and the image is rebuilt on the next call.  Writes through ``.data`` bypass the
+# version counter: call :func:`clear_packed_weights` after those.  Kept outside the modules (not
+# pickled, not deep-copied).
+_packed = weakref.WeakKeyDictionary()
+
+
+def clear_packed_weights() -> None:
+    _packed.clear()
+
+
+def packed_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> torch.Tensor:
+    """The ``mrp_edge_encoder_pack`` image of (W1, b1, W2), rebuilt when a weight changed."""
+    w1, b1, w2 = l1.weight, l1.bias, l2.weight
+    key = tuple((t.data_ptr(), t._version, t.device.index) for t in (w1, b1, w2))
+    hit = _packed.get(l2)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    C = w1.shape[0]
+    lib = _lib.load_library()
+    nbytes = int(lib.mrp_edge_encoder_pack_bytes(C))
+    img = torch.empty((nbytes + 3) // 4, device=w1.device, dtype=torch.float32)
+    w1c, b1c, w2c = (t.detach().contiguous().float() for t in (w1, b1, w2))
+    with torch.cuda.device(w1.device):
+        _lib.check(lib.mrp_edge_encoder_pack(_ptr(w1c), _ptr(b1c), _ptr(w2c), C, _ptr(img),
+                                             ctypes.c_void_p(torch.cuda.current_stream(w1.device).cuda_stream)),
+                   "mrp_edge_encoder_pack")
+    _packed[l2] = (key, img)
+    return img
+
+
+def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
+    """z = relu(pose W1^T + b1) W2^T + b2, (E, 2C), in one launch on the split-bf16 matrix cores
+    (``mrp_edge_encoder_fwd_split``); None when the kernel declines the shape (C % 32 != 0)."""
+    C = l1.weight.shape[0]
+    if not pose.is_cuda:
+        raise RuntimeError("mrp_gnn: the edge encoder kernel runs only on the GPU; no CPU fallback")
+    if C % 32 != 0 or tuple(l1.weight.shape) != (C, 9) or tuple(l2.weight.shape) != (2 * C, C) \
+            or l1.bias is None:
+        return None
+    img = packed_weights(l1, l2)
+    pose = pose.detach().contiguous().float()
+    b2 = l2.bias.detach().contiguous().float() if l2.bias is not None else None
+    E = pose.shape[0]
+    z = torch.empty((E, 2 * C), device=pose.device, dtype=torch.float32)
+    lib = _lib.load_library()
+    with torch.cuda.device(pose.device):
+        code = lib.mrp_edge_encoder_fwd_split(_ptr(pose), _ptr(img), _ptr(b2) if b2 is not None else None, E, C,
+                                              _ptr(z), ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream))
+    if code == _lib.HIP_ERROR_NOT_SUPPORTED:
+        return None
+    _lib.check(code, "mrp_edge_encoder_fwd_split")
+    return z
 
 
 def encoder_forward_fused(pose, w1, b1, w2, b2) -> torch.Tensor:
@@ -185,7 +245,12 @@ def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Te
     if not pose.is_cuda:
         raise RuntimeError("mrp_gnn: the edge encoder kernels run only on the GPU; no CPU fallback")
     params = (pose, l1.weight, l1.bias, l2.weight, l2.bias)
-    if _LOGITS_PATH == "fused" and not (torch.is_grad_enabled() and any(t.requires_grad for t in params)):
+    inference = not (torch.is_grad_enabled() and any(t.requires_grad for t in params))
+    if _LOGITS_PATH == "split" and inference:
+        z = encoder_forward_split(pose, l1, l2)
+        if z is not None:
+            return z
+    if _LOGITS_PATH == "fused" and inference:
         z = encoder_forward_fused(*params)
         if z is not None:
             return z

@@ -113,6 +113,19 @@ def test_edge_encoder_bwd_validation_without_launch():
     assert lib.mrp_edge_encoder_bwd(None, None, None, None, 8, 0, None, None, None, None, None) == 0  # C = 0: no-op
 
 
+def test_split_encoder_validation_without_launch():
+    lib = m.load_library()
+    # packed image: W1/b1 parts (C/32 x 3 x 64 lanes x 16 B) + W2 parts (2C/32 x C/32 x 2 x 3 x 64 x 16 B)
+    assert lib.mrp_edge_encoder_pack_bytes(512) == 512 * 96 + 2 * 512 * 512 * 6
+    assert lib.mrp_edge_encoder_pack_bytes(48) == 0 and lib.mrp_edge_encoder_pack_bytes(0) == 0
+    assert lib.mrp_edge_encoder_pack(None, None, None, 48, None, None) == m._lib.HIP_ERROR_NOT_SUPPORTED
+    assert lib.mrp_edge_encoder_pack(None, None, None, 64, None, None) == HIP_INVALID_VALUE
+    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 0, 64, None, None) == 0  # no edges: no-op
+    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 10, 48, None, None) == m._lib.HIP_ERROR_NOT_SUPPORTED
+    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 10, 64, None, None) == HIP_INVALID_VALUE
+    assert lib.mrp_edge_encoder_fwd_split(None, None, None, -1, 64, None, None) == HIP_INVALID_VALUE
+
+
 def test_tuning_knobs_documented_in_the_header():
     """mrp_tuning_set (host-only, no launch): every kernel-choice knob the header documents is accepted
     in range and rejected out of range; unknown names are rejected; "reset" restores defaults."""

@@ -148,9 +148,19 @@ def test_fused_encoder_equals_two_kernel_path(cuda_device, variant, E, C):
     assert ok, errs
 
 
+def _f64_logits(enc, pose):
+    with torch.no_grad():
+        t32 = enc.layers[2](torch.relu(enc.layers[0](pose)))
+        p64 = [t.detach().double() for t in enc.parameters()]
+        z64 = torch.nn.functional.linear(torch.relu(torch.nn.functional.linear(pose.double(), p64[0], p64[1])),
+                                         p64[2], p64[3])
+    return t32, z64
+
+
 def test_edge_logits_takes_fused_kernel_only_without_grad(cuda_device):
-    """edge_logits: inference -> the fused kernel; with gradients wanted -> the two-kernel autograd
-    path; a shape the fused kernel declines (C % 32) -> the two-kernel path (same values)."""
+    """edge_logits: inference -> the one-launch split-bf16 kernel; with gradients wanted -> the
+    two-kernel autograd path; a shape the kernel declines (C % 32) -> the two-kernel path.  Both
+    within the float64 yardstick of the reference layers."""
     torch.manual_seed(0)
     for C in (64, 48):
         enc = m.edge_encoder([C, C]).to(cuda_device)
@@ -159,4 +169,58 @@ def test_edge_logits_takes_fused_kernel_only_without_grad(cuda_device):
             z0 = m.encoder.edge_logits(enc.layers, pose)
         z1 = m.encoder.edge_logits(enc.layers, pose)
         assert z1.requires_grad and not z0.requires_grad
-        assert torch.allclose(z0, z1.detach(), rtol=1e-6, atol=1e-6)
+        t32, z64 = _f64_logits(enc, pose)
+        for z in (z0, z1.detach()):
+            ok, errs = stack_ref.within(z, t32, z64)
+            assert ok, errs
+
+
+@pytest.mark.parametrize("E,C", [(1, 32), (31, 32), (33, 64), (127, 96), (129, 128), (1792, 512), (448, 2048),
+                                 (300, 1024)])
+def test_split_encoder_vs_float64(cuda_device, E, C):
+    """mrp_edge_encoder_fwd_split (three-way bf16 split, six partial products) is as accurate as an fp32
+    evaluation of the reference layers (float64 yardstick), for ragged edge counts (partial 32-edge
+    waves and 128-edge workgroups), C from one hidden block to 64, poses of robot-scale magnitudes."""
+    torch.manual_seed(E * 3 + C)
+    enc = m.edge_encoder([C, C]).to(cuda_device)
+    pose = (torch.randn(E, 9) * 8).to(cuda_device)
+    with torch.no_grad():
+        z = m.encoder.encoder_forward_split(pose, enc.layers[0], enc.layers[2])
+    assert z is not None and z.shape == (E, 2 * C)
+    t32, z64 = _f64_logits(enc, pose)
+    ok, errs = stack_ref.within(z, t32, z64)
+    assert ok, errs
+
+
+def test_split_encoder_repacks_after_weight_update(cuda_device):
+    """The packed weight image follows optimizer updates (in-place, version-bumping) and is rebuilt
+    after clear_packed_weights() for writes through .data; a NULL bias b2 is accepted."""
+    torch.manual_seed(5)
+    C, E = 64, 200
+    enc = m.edge_encoder([C, C]).to(cuda_device)
+    pose = (torch.randn(E, 9) * 4).to(cuda_device)
+    l1, l2 = enc.layers[0], enc.layers[2]
+    with torch.no_grad():
+        z_a = m.encoder.encoder_forward_split(pose, l1, l2)
+        for p in enc.parameters():
+            p.mul_(1.5)  # what an optimizer step does: version bump
+        z_b = m.encoder.encoder_forward_split(pose, l1, l2)
+    t32, z64 = _f64_logits(enc, pose)
+    assert not torch.equal(z_a, z_b)
+    ok, errs = stack_ref.within(z_b, t32, z64)
+    assert ok, errs
+    l2.weight.data.mul_(-1.0)  # no version bump: needs the explicit clear
+    m.encoder.clear_packed_weights()
+    with torch.no_grad():
+        z_c = m.encoder.encoder_forward_split(pose, l1, l2)
+    t32, z64 = _f64_logits(enc, pose)
+    ok, errs = stack_ref.within(z_c, t32, z64)
+    assert ok, errs
+    img = m.encoder.packed_weights(l1, l2)
+    zn = torch.empty(E, 2 * C, device=cuda_device)
+    lib = m.load_library()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    assert lib.mrp_edge_encoder_fwd_split(p(pose), p(img), None, E, C, p(zn), ctypes.c_void_p(0)) == 0
+    torch.cuda.synchronize()
+    assert rel_err((zn + l2.bias).detach().cpu().numpy(), z_c.cpu().numpy()) <= 1e-6
+    assert lib.mrp_edge_encoder_pack_bytes(48) == 0

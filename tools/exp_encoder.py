@@ -1,6 +1,7 @@
 """Kernel lab (not product code): the edge encoder's second Linear z = h W2^T + b2 — the matrix-core
 kernel mrp_edge_logits_fwd (mrp_tuning_set "edge_gemm" 0 / 1) against torch.addmm (hipBLASLt) —
-the one-launch encoder mrp_edge_encoder_fwd ("edge_fused" 0..4), and the whole encoder forward per
+the one-launch encoder mrp_edge_encoder_fwd ("edge_fused" 0..4), its split-bf16 form
+mrp_edge_encoder_fwd_split, and the whole encoder forward per
 path (library / hidden + logits kernels / fused), HIP-graph timed (bench.time_launches), at
 the headline size (B = 32 complete graphs of 8: E = 1792, C = 512) and the BASELINE configs.
 
@@ -58,7 +59,11 @@ for name, E, C in SHAPES:
             t = time_launches([lambda: enc.encoder_forward_fused(*args_f)], args.iters, dev)
             row.append(f"fused{v} {t * 1e6:6.1f} us{'' if same else ' MISMATCH'}")
         lib.mrp_tuning_set(b"reset", 0)
-        for path in ("library", "hip", "fused"):
+        zs = enc.encoder_forward_split(pose, l1, layers[2])
+        err = float((zs - ref_full).abs().max() / ref_full.abs().max())
+        t = time_launches([lambda: enc.encoder_forward_split(pose, l1, layers[2])], args.iters, dev)
+        row.append(f"split {t * 1e6:6.1f} us (vs fused {err:.1e})")
+        for path in ("library", "hip", "fused", "split"):
             enc.set_logits_path(path)
             t = time_launches([lambda: enc.edge_logits(layers, pose)], args.iters, dev)
             row.append(f"encoder[{path}] {t * 1e6:6.1f} us")
