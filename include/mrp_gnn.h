@@ -339,7 +339,8 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * backward, 1 or 2), "bwd_pre2", "fwd_regular_split" (0, default: whole planes); compress GEMM
  * kernel variants "gemm_nn" / "gemm_nt" (-1, default: the per-shape choice; 0..5: compress_gemm.hip's
  * variant table); "edge_gemm" (1, default: mrp_edge_logits_fwd on 32x32x2 MFMAs; 0: 16x16x4); "edge_fused"
- * (mrp_edge_encoder_fwd tile/buffer variant, 0..4). */
+ * (mrp_edge_encoder_fwd tile/buffer variant, 0..4); "edge_split_cb" (mrp_edge_encoder_fwd_split: 32-column
+ * blocks per wave, 1 or 2 (default)). */
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 14 = this header: v13 plus

@@ -33,6 +33,7 @@
 #include <stdint.h>
 
 #include "mrp_gnn.h"
+#include "tuning.hpp"
 
 namespace mrp_x6 {
 
@@ -148,19 +149,40 @@ struct FwdArgs {
 };
 
 // LDS stage of one hidden block, shared by the workgroup's four waves (one per 32-edge block, one
-// column slab): 16 pieces of 1 KiB (64 lanes x 16 B, a lane's fragment at 16 lane): pieces 0..11 the
-// W2 parts of the slab's two column blocks (c, s, p) = 6 c + 3 s + p, 12..14 the W1 parts, 15 a copy
-// of 14 (so every wave issues exactly four LDS-DMA pieces per stage and counts them alike).
-constexpr int kPieces = 16, kStageU4 = kPieces * 64, kStages = 4;
+// column slab of CB column blocks): NP = 6 CB + 3 pieces of 1 KiB (64 lanes x 16 B, a lane's fragment
+// at 16 lane): pieces 0 .. 6 CB - 1 the W2 parts (c, s, p) = 6 c + 3 s + p, then the 3 W1 parts.
+// Piece pc is DMA'd by wave pc % 4.
+template <int CB>
+struct Stage {
+  static constexpr int NP = 6 * CB + 3;
+  static constexpr int U4 = NP * 64;   // 16-B units per stage
+  static constexpr int PW = (NP + 3) / 4;  // most pieces a wave issues per stage
+};
+constexpr int kStages = 4;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
 
-__global__ void __launch_bounds__(256) encoder_fwd(FwdArgs a) {
+// s_waitcnt vmcnt(n) for a wave-uniform n <= 4 (the immediate must be a constant)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+  }
+}
+
+template <int CB>
+__device__ __forceinline__ void encoder_body(const FwdArgs& a) {
+  using S = Stage<CB>;
+  constexpr int NF = S::NP;  // fragments per stage
+  constexpr int W1F = 6 * CB;  // first W1 fragment
   extern __shared__ u4 lds[];
-  // workgroup -> (edge group of 128, column slab of 64); consecutive ids share a slab (its W2 image)
-  // and, after the remap, an XCD and its L2
+  // workgroup -> (edge group of 128, column slab of 32 CB); consecutive ids share a slab (its W2
+  // image) and, after the remap, an XCD and its L2
   const int nwg = gridDim.x;
   const int orig = blockIdx.x;
   const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
@@ -172,30 +194,31 @@ __global__ void __launch_bounds__(256) encoder_fwd(FwdArgs a) {
   const int HB = a.C / 32;
   const int r = lane & 31, hh = lane >> 5;
 
-  // ---- LDS-DMA: wave wv issues pieces 4 wv .. 4 wv + 3 of every stage
+  // ---- LDS-DMA: wave wv issues pieces wv, wv + 4, ... of every stage (npw of them)
+  const int npw = (S::NP - wv + 3) / 4;
   const int64_t cstride = (int64_t)HB * 2 * 3 * 64;  // 16-B units per W2 column block
   const __amdgpu_buffer_rsrc_t rw = rsrc(a.packed);
-  uint32_t voff[4];
+  uint32_t voff[S::PW], sstep[S::PW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int pc = 4 * wv + i;
-    int64_t unit;  // the piece's first unit at hidden block 0
-    if (pc < 12) {
+  for (int i = 0; i < S::PW; ++i) {
+    const int pc = wv + 4 * i;
+    int64_t unit;  // the piece's first unit at hidden block 0, and its advance per hidden block
+    if (pc < W1F) {
       const int c = pc / 6, sp = pc % 6;  // sp = 3 s + p
-      unit = w1_units(a.C) + (int64_t)(2 * cs + c) * cstride + sp * 64;
+      unit = w1_units(a.C) + (int64_t)(CB * cs + c) * cstride + sp * 64;
+      sstep[i] = 6 * 64 * 16;
     } else {
-      unit = (int64_t)(pc < 15 ? pc - 12 : 2) * 64;
+      unit = (int64_t)(pc < NF ? pc - W1F : 0) * 64;
+      sstep[i] = 3 * 64 * 16;
     }
     voff[i] = (uint32_t)((unit + lane) * 16);
   }
   auto issue = [&](int hb) {
-    u4* st = lds + (hb % kStages) * kStageU4;
+    u4* st = lds + (hb % kStages) * S::U4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int pc = 4 * wv + i;
-      const uint32_t soff = (uint32_t)(hb * (pc < 12 ? 6 * 64 : 3 * 64) * 16);  // per hidden block
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, st + pc * 64, 16, voff[i], soff, 0, 0);
-    }
+    for (int i = 0; i < S::PW; ++i)
+      if (i < npw)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, st + (wv + 4 * i) * 64, 16, voff[i], (uint32_t)hb * sstep[i], 0, 0);
   };
   // pose fragment (B operand of X = W1' pose'^T): lane's edge, k = 8 hh + j; k = 9 is the 1.0 of b1
   bf8 pp[3];
@@ -218,9 +241,9 @@ __global__ void __launch_bounds__(256) encoder_fwd(FwdArgs a) {
   issue(0);
   if (HB > 1) issue(1);
 
-  f16v Z[2];
+  f16v Z[CB];
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c < CB; ++c)
 #pragma unroll
     for (int i = 0; i < 16; ++i) Z[c][i] = 0.f;
   bf8 hp[2][3];  // the previous block's ReLU'd hidden values, split (A operand per 16-unit step)
@@ -228,25 +251,22 @@ __global__ void __launch_bounds__(256) encoder_fwd(FwdArgs a) {
   // Stage hb landed (own pieces; the younger stage hb + 1 may still be in flight), then the barrier
   // publishes every wave's pieces and certifies that all reads of the previous iteration are done.
   auto stage_ready = [&](int hb) {
-    if (hb + 1 < HB)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_vmcnt(hb + 1 < HB ? npw : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
-  // a stage's fragments into registers: W1 parts first (X needs them first), then the 12 W2 parts
-  auto read_frags = [&](int hb, u4 (&w)[15]) {
-    const u4* st = lds + (hb % kStages) * kStageU4 + lane;
+  // a stage's fragments into registers: W1 parts first (X needs them first), then the W2 parts
+  auto read_frags = [&](int hb, u4 (&w)[NF]) {
+    const u4* st = lds + (hb % kStages) * S::U4 + lane;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) w[12 + k] = st[(12 + k) * 64];
+    for (int k = 0; k < 3; ++k) w[W1F + k] = st[(W1F + k) * 64];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) w[k] = st[k * 64];
+    for (int k = 0; k < W1F; ++k) w[k] = st[k * 64];
   };
-  auto x_block = [&](const u4 (&w)[15]) {  // X = W1' pose'^T
+  auto x_block = [&](const u4 (&w)[NF]) {  // X = W1' pose'^T
     bf8 wa[3];
 #pragma unroll
-    for (int p = 0; p < 3; ++p) wa[p] = as_bf8(w[12 + p]);
+    for (int p = 0; p < 3; ++p) wa[p] = as_bf8(w[W1F + p]);
     f16v X;
 #pragma unroll
     for (int i = 0; i < 16; ++i) X[i] = 0.f;
@@ -261,11 +281,11 @@ __global__ void __launch_bounds__(256) encoder_fwd(FwdArgs a) {
       split8(hv, hp[s]);
     }
   };
-  auto z_block = [&](const u4 (&w)[15]) {  // z += relu(X)^T W2^T (hp holds relu(X) split)
+  auto z_block = [&](const u4 (&w)[NF]) {  // z += relu(X)^T W2^T (hp holds relu(X) split)
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < CB; ++c) {
         bf8 wb[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) wb[p] = as_bf8(w[6 * c + 3 * s + p]);
@@ -277,8 +297,8 @@ __global__ void __launch_bounds__(256) encoder_fwd(FwdArgs a) {
   // stage hb's fragments into registers (in flight) while the matrix cores run X of block hb (its W1
   // fragments are read first) and z of block hb - 1 (fragments already in registers), then X's ReLU
   // and split on the VALU.
-  u4 F[15], G[15];
-  auto step = [&](int hb, u4 (&cur)[15], u4 (&nxt)[15]) {  // cur: stage hb - 1's fragments
+  u4 F[NF], G[NF];
+  auto step = [&](int hb, u4 (&cur)[NF], u4 (&nxt)[NF]) {  // cur: stage hb - 1's fragments
     stage_ready(hb);
     if (hb + 2 < HB) issue(hb + 2);
     read_frags(hb, nxt);
@@ -299,7 +319,7 @@ __global__ void __launch_bounds__(256) encoder_fwd(FwdArgs a) {
   if (hb < HB) {
     step(hb, F, G);
 #pragma unroll
-    for (int k = 0; k < 15; ++k) F[k] = G[k];
+    for (int k = 0; k < NF; ++k) F[k] = G[k];
   }
   z_block(F);
 
@@ -307,8 +327,8 @@ __global__ void __launch_bounds__(256) encoder_fwd(FwdArgs a) {
   if (e0 >= a.E) return;  // a wave past the last edge (only the stores are skipped: it took part in the barriers)
   const int N = 2 * a.C;
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int col = (2 * cs + c) * 32 + r;
+  for (int c = 0; c < CB; ++c) {
+    const int col = (CB * cs + c) * 32 + r;
     const float bias = a.b2 != nullptr ? a.b2[col] : 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -316,6 +336,18 @@ __global__ void __launch_bounds__(256) encoder_fwd(FwdArgs a) {
       if (e < a.E) a.z[(int64_t)e * N + col] = __fadd_rn(Z[c][i], bias);
     }
   }
+}
+
+// one kernel per column-block count (plain kernels around the template body)
+__global__ void __launch_bounds__(256) encoder_fwd_cb1(FwdArgs a) { encoder_body<1>(a); }
+__global__ void __launch_bounds__(256) encoder_fwd_cb2(FwdArgs a) { encoder_body<2>(a); }
+
+hipError_t launch_fwd(int cb, const FwdArgs& a, int64_t grid, hipStream_t st) {
+  if (cb == 2)
+    hipLaunchKernelGGL(encoder_fwd_cb2, dim3((unsigned)grid), dim3(256), (size_t)kStages * Stage<2>::U4 * 16, st, a);
+  else
+    hipLaunchKernelGGL(encoder_fwd_cb1, dim3((unsigned)grid), dim3(256), (size_t)kStages * Stage<1>::U4 * 16, st, a);
+  return hipGetLastError();
 }
 
 }  // namespace mrp_x6
@@ -353,9 +385,10 @@ extern "C" int mrp_edge_encoder_fwd_split(const float* pose, const void* packed,
   a.E = num_edges;
   a.C = C;
   a.egroups = (num_edges + 127) / 128;
-  const int64_t grid = (int64_t)a.egroups * (2 * (int64_t)C / 64);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // column blocks per wave: 1 (two workgroups per CU, X recomputed per 32 columns) or 2 (one per CU)
+  const int cb = mrp_host::tuning().edge_split_cb == 2 ? 2 : 1;
+  const int64_t grid = (int64_t)a.egroups * (2 * (int64_t)C / (32 * cb));
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  constexpr size_t lds = (size_t)kStages * kStageU4 * 16;  // 64 KiB
-  hipLaunchKernelGGL(encoder_fwd, dim3((unsigned)grid), dim3(256), lds, static_cast<hipStream_t>(stream), a);
-  return hipGetLastError();
+  return launch_fwd(cb, a, grid, st);
 }

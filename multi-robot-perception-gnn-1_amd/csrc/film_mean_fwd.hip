@@ -107,6 +107,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"gemm_nt", &t.gemm_nt, -1, 5},
       {"edge_gemm", &t.edge_gemm, 0, 1},
       {"edge_fused", &t.edge_fused, 0, 4},
+      {"edge_split_cb", &t.edge_split_cb, 1, 2},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {

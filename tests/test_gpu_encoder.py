@@ -177,15 +177,22 @@ def test_edge_logits_takes_fused_kernel_only_without_grad(cuda_device):
 
 @pytest.mark.parametrize("E,C", [(1, 32), (31, 32), (33, 64), (127, 96), (129, 128), (1792, 512), (448, 2048),
                                  (300, 1024)])
-def test_split_encoder_vs_float64(cuda_device, E, C):
-    """mrp_edge_encoder_fwd_split (three-way bf16 split, six partial products) is as accurate as an fp32
-    evaluation of the reference layers (float64 yardstick), for ragged edge counts (partial 32-edge
-    waves and 128-edge workgroups), C from one hidden block to 64, poses of robot-scale magnitudes."""
+@pytest.mark.parametrize("cb", [1, 2])
+def test_split_encoder_vs_float64(cuda_device, E, C, cb):
+    """mrp_edge_encoder_fwd_split (three-way bf16 split, six partial products; one or two 32-column
+    blocks per wave) is as accurate as an fp32 evaluation of the reference layers (float64
+    yardstick), for ragged edge counts (partial 32-edge waves and 128-edge workgroups), C from one
+    hidden block to 64, poses of robot-scale magnitudes."""
     torch.manual_seed(E * 3 + C)
     enc = m.edge_encoder([C, C]).to(cuda_device)
     pose = (torch.randn(E, 9) * 8).to(cuda_device)
-    with torch.no_grad():
-        z = m.encoder.encoder_forward_split(pose, enc.layers[0], enc.layers[2])
+    lib = m.load_library()
+    assert lib.mrp_tuning_set(b"edge_split_cb", cb) == 0
+    try:
+        with torch.no_grad():
+            z = m.encoder.encoder_forward_split(pose, enc.layers[0], enc.layers[2])
+    finally:
+        lib.mrp_tuning_set(b"reset", 0)
     assert z is not None and z.shape == (E, 2 * C)
     t32, z64 = _f64_logits(enc, pose)
     ok, errs = stack_ref.within(z, t32, z64)
