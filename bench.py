@@ -407,13 +407,14 @@ def config_record(cid, world, rank, device, args):
             reducer.synchronize()
 
     prev = mrp.compress.compress_path()
-    times = {(k, path): [] for k in ("fwd", "train") for path in ("hip", "library")}
+    product = prev  # the package default ("split": split-bf16 forward / data gradient)
+    times = {(k, path): [] for k in ("fwd", "train") for path in (product, "library")}
     try:
         for _ in range(2):
             fwd()
             train()
         for _ in range(3):
-            for path in ("hip", "library"):
+            for path in (product, "library"):
                 mrp.compress.set_compress_path(path)
                 for k, fn in (("fwd", fwd), ("train", train)):
                     for _ in range(2):
@@ -422,10 +423,10 @@ def config_record(cid, world, rank, device, args):
     finally:
         mrp.compress.set_compress_path(prev)
     med = {k: sorted(v)[1] for k, v in times.items()}
-    t, tt = med[("fwd", "hip")], med[("train", "hip")]
+    t, tt = med[("fwd", product)], med[("train", product)]
     rec["forward"] = {"value": world * elems / t if scaling == "weak" else None, "unit": "elems/s",
                       "ms_per_step": t * 1e3,
-                      "compress": "aggregate kernel + matrix-core compress kernel (no cat buffer)",
+                      "compress": f"aggregate kernel + matrix-core compress kernels, path {product!r} (no cat buffer)",
                       "ms_per_step_library_compress": med[("fwd", "library")] * 1e3}
     if scaling == "strong":  # every rank holds a different part of one global batch
         tot = torch.tensor([float(elems)], dtype=torch.float64,

@@ -247,6 +247,31 @@ int mrp_compress_bwd_weight(const float* gy, int64_t gy_node_stride, const float
                             float* gw, float* gbias, void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
+ * The compress forward and data gradient on the bf16 matrix cores at fp32 accuracy
+ * (compress_split.hip): the same products as mrp_compress_fwd / mrp_compress_bwd_data, each fp32
+ * operand split exactly into three bf16 parts and each product the sum of the six partial products
+ * whose omitted terms are below 2^-25 of it (error against float64 at or below an fp32 GEMM's).  The
+ * weight operand is split and laid out once per weight version:
+ *   mrp_compress_split_pack_bytes(M, K)   bytes of a packed M x K operand (0 unless M % 32 == 0, K % 16 == 0)
+ *   mrp_compress_split_pack(w, ld, transpose, M, K, packed)
+ *                                         A = w (M x K row-major, row stride ld) or, transpose != 0,
+ *                                         A = w^T (w: K x M row-major, row stride ld) -> packed (16-byte aligned)
+ *   mrp_compress_fwd_split                y = W [x; agg] + b with packed = pack(w, 2C, 0, C, 2C)
+ *   mrp_compress_bwd_data_split           [gx; gagg] = W^T gy with packed = pack(w, 2C, 1, 2C, C)
+ * Arguments otherwise as mrp_compress_fwd / mrp_compress_bwd_data.  Requirements (else
+ * hipErrorNotSupported): C % 32 == 0, P % 4 == 0, x / agg / gy 16-byte aligned with node strides % 4 == 0.
+ */
+int64_t mrp_compress_split_pack_bytes(int32_t M, int32_t K);
+int mrp_compress_split_pack(const float* w, int64_t ld, int32_t transpose, int32_t M, int32_t K, void* packed,
+                            void* stream);
+int mrp_compress_fwd_split(const float* x, int64_t x_node_stride, const float* agg, int64_t agg_node_stride,
+                           int32_t num_nodes, int32_t C, int32_t P, const void* packed_w, const float* bias, float* y,
+                           int64_t y_node_stride, void* stream);
+int mrp_compress_bwd_data_split(const float* gy, int64_t gy_node_stride, int32_t num_nodes, int32_t C, int32_t P,
+                                const void* packed_wt, float* gx, int64_t gx_node_stride, float* gagg,
+                                int64_t gagg_node_stride, void* stream);
+
+/*
  * First layer of the edge encoder, dgl/model/models.py:147-148:  h = relu(pose W1^T + b1).
  *   pose (num_edges, 9), w1 (C, 9) (nn.Linear weight layout), b1 (C) -> h (num_edges, C), fp32.
  * The second Linear is mrp_edge_logits_fwd and its Sigmoid is fused into the aggregation
@@ -340,10 +365,13 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * kernel variants "gemm_nn" / "gemm_nt" (-1, default: the per-shape choice; 0..5: compress_gemm.hip's
  * variant table); "edge_gemm" (1, default: mrp_edge_logits_fwd on 32x32x2 MFMAs; 0: 16x16x4); "edge_fused"
  * (mrp_edge_encoder_fwd tile/buffer variant, 0..4); "edge_split_cb" (mrp_edge_encoder_fwd_split: 32-column
- * blocks per wave, 1 or 2 (default)). */
+ * blocks per wave, 1 or 2 (default)); "gemm_split" (split-bf16 compress GEMM workgroup: -1 per shape,
+ * 2 = 128 rows / 4 waves, 4 = 256 rows / 8 waves). */
 int mrp_tuning_set(const char* name, int32_t value);
 
-/* Library identification: ABI version (incremented on signature changes; 14 = this header: v13 plus
+/* Library identification: ABI version (incremented on signature changes; 15 = this header: v14 plus
+ * the split-bf16 compress forward / data gradient and their weight packing (mrp_compress_split_*,
+ * mrp_compress_fwd_split, mrp_compress_bwd_data_split); 14: v13 plus
  * the split-bf16 edge encoder forward and its weight packing (mrp_edge_encoder_pack_bytes /
  * _pack / _fwd_split); 13: the
  * aggregation and epilogue entry points of v10, the matrix-core compress forward and gradients,

@@ -12,7 +12,8 @@ REPO = os.path.dirname(PKG_DIR)
 SOURCES = [os.path.join(PKG_DIR, "csrc", f) for f in ("film_mean_fwd.hip", "film_mean_bwd.hip", "film_mean_bwd_1_8.hip",
                                                     "film_mean_bwd_9_12.hip", "film_mean_bwd_13_16.hip",
                                                     "edge_encoder.hip", "frame_graph.hip",
-                                                    "compress_gemm.hip", "encoder_split.hip")]
+                                                    "compress_gemm.hip", "encoder_split.hip",
+                                                    "compress_split.hip")]
 OBJ_DIR = os.path.join(PKG_DIR, "build")
 HEADERS = [os.path.join(REPO, "include", "mrp_gnn.h")] + [os.path.join(PKG_DIR, "csrc", h) for h in (
     "film_mean_kernels.hpp", "film_mean_bwd_launch.hpp", "fast_math.hpp", "tuning.hpp")]

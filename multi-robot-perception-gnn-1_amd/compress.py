@@ -1,7 +1,6 @@
 """The 1x1 compress convolution after the concatenation (``dgl/model/models.py:163-165,181-184,186-189``:
 ``h = conv(torch.cat((h, g_h), 1))`` with ``conv = nn.Conv2d(2C, C, kernel_size=1)``) and both of its
-gradients on the hand-written fp32 matrix-core kernels of ``csrc/compress_gemm.hip``
-(``include/mrp_gnn.h``: ``mrp_compress_fwd``, ``mrp_compress_bwd_data``, ``mrp_compress_bwd_weight``).
+gradients on hand-written matrix-core kernels (``include/mrp_gnn.h``).
 
 Per node n a 1x1 convolution over NCHW is ``y[n] = W [x[n]; a[n]] + b`` with W (C, 2C) shared, so:
 
@@ -12,30 +11,78 @@ Per node n a 1x1 convolution over NCHW is ``y[n] = W [x[n]; a[n]] + b`` with W (
 * weight grad:  ``dW = sum_n dy[n] [x[n]; a[n]]^T`` and ``db = sum dy`` in one split-K kernel with a
   fixed-order sum of its partial tiles (deterministic), no (N, C, 2C) temporary, no layout copies.
 
+Arithmetic (:func:`set_compress_path`): ``"split"`` (default) runs the forward and the data gradient on
+the bf16 matrix cores with every fp32 operand split exactly into three bf16 parts and six partial
+products per product (``mrp_compress_fwd_split`` / ``mrp_compress_bwd_data_split``, as accurate as an
+fp32 GEMM: the omitted terms are below 2^-25 of each product) and the weight gradient on the fp32 MFMA;
+``"hip"`` runs all three on the fp32 MFMA (``mrp_compress_fwd`` / ``_bwd_data`` / ``_bwd_weight``, exact
+fp32 products).  Both are checked against float64 (``tests/stack_ref``).  The split weight images are
+built once per weight version (:func:`packed_weight`).
+
 The module keeps the reference's ``nn.Conv2d`` parameters (``conv1.weight`` (C, 2C, 1, 1),
-``conv1.bias``), so ``state_dict`` keys are unchanged.  Same fp32 arithmetic as the convolution
-(exact fp32 products), different summation order: checked against float64 (``tests/stack_ref``).
+``conv1.bias``), so ``state_dict`` keys are unchanged.
 
 Shapes the kernels decline (C % 32 != 0, H W % 4 != 0 — and, for the weight gradient only,
 H W % 32 != 0 — none of them a reference configuration: the reference's planes are
 ``image_size/32`` squares, 8 x 8 at its default) run torch's own GEMMs
-(:func:`set_compress_path` ``"library"`` forces that path everywhere, for A/B measurements).
+(``set_compress_path("library")`` forces that path everywhere, for A/B measurements).
 """
 from __future__ import annotations
+
+import weakref
 
 import torch
 
 from . import _lib
 
-_PATH = ["hip"]
+_PATH = ["split"]
 
 
 def set_compress_path(path: str) -> None:
-    """``"hip"`` (default): the matrix-core kernels above; ``"library"``: the cat kernel + torch's
-    library GEMMs (the round-2 path), for A/B measurement."""
-    if path not in ("hip", "library"):
-        raise ValueError("compress path must be 'hip' or 'library'")
+    """``"split"`` (default): forward and data gradient on the split-bf16 matrix cores
+    (``compress_split.hip``, fp32-accurate), weight gradient on the fp32 MFMA; ``"hip"``: all three on
+    the fp32 MFMA (``compress_gemm.hip``); ``"library"``: the cat kernel + torch's library GEMMs (the
+    round-2 path), for A/B measurement."""
+    if path not in ("split", "hip", "library"):
+        raise ValueError("compress path must be 'split', 'hip' or 'library'")
     _PATH[0] = path
+
+
+# packed split-bf16 images of a compress weight, per weight tensor: id -> (weakref, {"fwd" | "bwd":
+# (key, image)}), dropped when the tensor dies (tensors compare elementwise, so no WeakKeyDictionary).
+# The key holds the data pointer and autograd version, so an optimizer step (an in-place update under
+# no_grad) triggers a repack; writes through ``.data`` bypass the version counter: call
+# :func:`clear_packed_weights` after those.  Kept outside the modules (not pickled, not deep-copied).
+_packed = {}
+
+
+def clear_packed_weights() -> None:
+    _packed.clear()
+
+
+def packed_weight(weight: torch.Tensor, kind: str) -> torch.Tensor:
+    """``mrp_compress_split_pack`` image of the (C, 2C[, 1, 1]) weight: ``"fwd"`` packs W (M = C,
+    K = 2C) for the forward, ``"bwd"`` packs W^T (M = 2C, K = C) for the data gradient."""
+    from .aggregate import _ptr, _stream
+    key = (weight.data_ptr(), weight._version, weight.device.index)
+    entry = _packed.get(id(weight))
+    slot = entry[1] if entry is not None and entry[0]() is weight else None
+    if slot is not None and kind in slot and slot[kind][0] == key:
+        return slot[kind][1]
+    C = weight.shape[0]
+    w = _weight2d(weight)
+    M, K, trans = (C, 2 * C, 0) if kind == "fwd" else (2 * C, C, 1)
+    lib = _lib.load_library()
+    img = torch.empty((int(lib.mrp_compress_split_pack_bytes(M, K)) + 3) // 4, device=w.device, dtype=torch.float32)
+    with torch.cuda.device(w.device):
+        _lib.check(lib.mrp_compress_split_pack(_ptr(w), 2 * C, trans, M, K, _ptr(img), _stream(w.device)),
+                   "mrp_compress_split_pack")
+    if slot is None:
+        slot = {}
+        wid = id(weight)
+        _packed[wid] = (weakref.ref(weight, lambda _r, wid=wid: _packed.pop(wid, None)), slot)
+    slot[kind] = (key, img)
+    return img
 
 
 def compress_path() -> str:
@@ -91,9 +138,15 @@ def compress_forward(weight: torch.Tensor, bias, x: torch.Tensor, a: torch.Tenso
     if b is not None and (b.dtype != torch.float32 or not b.is_contiguous()):
         b = b.float().contiguous()
     y = torch.empty((n, C, H, W), device=x.device, dtype=torch.float32)
+    lib = _lib.load_library()
     with torch.cuda.device(x.device):
-        _lib.check(_lib.load_library().mrp_compress_fwd(_ptr(x), xs, _ptr(a), as_, n, C, H * W, _ptr(w), _ptr(b),
-                                                        _ptr(y), C * H * W, _stream(x.device)), "mrp_compress_fwd")
+        if _PATH[0] == "split":
+            img = packed_weight(weight, "fwd")
+            _lib.check(lib.mrp_compress_fwd_split(_ptr(x), xs, _ptr(a), as_, n, C, H * W, _ptr(img), _ptr(b), _ptr(y),
+                                                  C * H * W, _stream(x.device)), "mrp_compress_fwd_split")
+        else:
+            _lib.check(lib.mrp_compress_fwd(_ptr(x), xs, _ptr(a), as_, n, C, H * W, _ptr(w), _ptr(b), _ptr(y),
+                                            C * H * W, _stream(x.device)), "mrp_compress_fwd")
     return y
 
 
@@ -104,8 +157,6 @@ def compress_backward_data(weight: torch.Tensor, gy: torch.Tensor, gx: torch.Ten
     n, C, H, W = gy.shape
     lib = _lib.load_library()
     gy, gs = _node_major(gy)
-    w = _weight2d(weight)
-    wt = torch.empty((2 * C, C), device=gy.device, dtype=torch.float32)
     gx = torch.empty((n, C, H, W), device=gy.device, dtype=torch.float32) if gx is None else gx
     ga = torch.empty((n, C, H, W), device=gy.device, dtype=torch.float32) if ga is None else ga
     gxs, gas = _nstride(gx), _nstride(ga)
@@ -113,6 +164,13 @@ def compress_backward_data(weight: torch.Tensor, gy: torch.Tensor, gx: torch.Ten
         raise ValueError("compress_backward_data: outputs must be node-major fp32, 16-byte aligned")
     st = _stream(gy.device)
     with torch.cuda.device(gy.device):
+        if _PATH[0] == "split":
+            img = packed_weight(weight, "bwd")
+            _lib.check(lib.mrp_compress_bwd_data_split(_ptr(gy), gs, n, C, H * W, _ptr(img), _ptr(gx), gxs, _ptr(ga),
+                                                       gas, st), "mrp_compress_bwd_data_split")
+            return gx, ga
+        w = _weight2d(weight)
+        wt = torch.empty((2 * C, C), device=gy.device, dtype=torch.float32)
         _lib.check(lib.mrp_compress_weight_transpose(_ptr(w), _ptr(wt), C, st), "mrp_compress_weight_transpose")
         _lib.check(lib.mrp_compress_bwd_data(_ptr(gy), gs, n, C, H * W, _ptr(wt), _ptr(gx), gxs, _ptr(ga), gas, st),
                    "mrp_compress_bwd_data")
@@ -167,7 +225,7 @@ def _lib_backward_weight(gy, x, a, want_bias):
 
 
 def _use_kernels(C, P) -> bool:
-    return _PATH[0] == "hip" and kernels_supported(C, P)
+    return _PATH[0] in ("hip", "split") and kernels_supported(C, P)
 
 
 class CompressFunction(torch.autograd.Function):

@@ -1,0 +1,409 @@
+// compress_split.hip — the GCN layer's 1x1 compress convolution (forward and data gradient) on the
+// bf16 matrix cores at fp32 accuracy, gfx950 (MI355X / CDNA4).
+//
+// Reference (xjh19971/multi-robot-perception-gnn-1, dgl/model/models.py:163-165,181-184,186-189):
+//     h = self.conv1(torch.cat((h, g_h), dim=1))       # nn.Conv2d(2C, C, kernel_size=1), fp32
+// and its input gradient in training (dgl/training.py:208-210).  Per node n, with P = H W pixels:
+//     forward      y[n] = W [x[n]; a[n]] + b          M = C,  K = 2C (rows from x, then a)
+//     data grad    [dx[n]; da[n]] = W^T dy[n]         M = 2C, K = C  (rows to dx, then da)
+// the same NN product as compress_gemm.hip's gemm_nn (which runs it on the fp32 MFMA), here on
+// v_mfma_f32_32x32x16_bf16 with the exact three-way bf16 split of encoder_split.hip: every fp32 operand
+// x = x0 + x1 + x2 (+ < 2^-24 |x|), each product the sum of the six partial products a_i b_j with
+// i + j <= 2, exact in the MFMA and summed in fp32 — as accurate as an fp32 GEMM (the omitted terms are
+// below 2^-25 of the product; 6 roundings per 16 k against the fp32 MFMA's 16), at 192 MFMA cycles per
+// 16 k instead of 512.
+//
+// Operands.  A (the weight, M x K) is split and laid out once per weight version by
+// mrp_compress_split_pack in per-lane fragment order (16-byte unit ((mb KS + ks) 3 + p) 64 + lane holds
+// lane (r, h)'s eight k = 16 ks + 8 h + j of row 32 mb + r, part p) and arrives by LDS-DMA.  B (the
+// activations) is node-major NCHW: k = channel rows of P contiguous pixels, i.e. k-strided for the
+// MFMA, which wants eight consecutive k per lane.  Each thread loads 16-byte row pieces of the next
+// stage into registers, splits them, and stores the three bf16 parts row-major into LDS ([k][column],
+// 256-byte rows, 16-byte chunks XOR-swizzled by the row: cdna_hip_programming.md T10 layout (b)); the
+// MFMA fragments come back with ds_read_b64_tr_b16, which delivers four k of one column per lane
+// (conflict-free on that layout).
+//
+// Workgroup: a (64 WMW) x 128 output tile of WMW x 2 waves of 64 x 64 (2 x 2 blocks of 32 x 32), WMW = 2
+// (4 waves) or 4 (8 waves: two per SIMD, and each B stage split once for 256 rows); K in stages of 32
+// (two 16-k MFMA steps), two LDS buffers (A 12 WMW KiB + B 3 x 8 KiB each): stage s + 1's A is DMA'd
+// and its B loaded into registers while stage s is multiplied; one barrier per stage.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mrp_gnn.h"
+#include "tuning.hpp"
+
+namespace mrp_cs {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+
+constexpr int TN = 128, BK = 32;
+constexpr int B_PART_BYTES = BK * TN * 2;  // one bf16 part of the B stage: 8 KiB
+
+// Workgroup geometry: WMW x 2 waves of 64 x 64, TM = 64 WMW rows.
+template <int WMW>
+struct Geo {
+  static constexpr int TM = 64 * WMW, NW = 2 * WMW, THREADS = 64 * NW;
+  static constexpr int A_PIECES = (TM / 32) * (BK / 16) * 3;  // 1 KiB pieces per stage (6 per wave)
+  static constexpr int A_BYTES = A_PIECES * 1024;
+  static constexpr int BUF_BYTES = A_BYTES + 3 * B_PART_BYTES;
+  static constexpr int LDS_BYTES = 2 * BUF_BYTES;  // 96 KiB (WMW 2), 144 KiB (WMW 4)
+  static constexpr int BJ = BK * TN / 4 / THREADS;  // 16-byte B pieces per thread per stage
+  static constexpr int KR = THREADS / 32;           // B rows per pass
+};
+
+__device__ __forceinline__ uint32_t cvt2(f2 x) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(x, bf2)); }
+__device__ __forceinline__ f2 widen2(uint32_t p) {
+  f2 r;
+  r.x = __uint_as_float(p << 16);
+  r.y = __uint_as_float(p & 0xffff0000u);
+  return r;
+}
+
+// exact three-way split of two fp32 values: one dword (two bf16) per part
+__device__ __forceinline__ void split2(f2 x, uint32_t& a, uint32_t& b, uint32_t& c) {
+  a = cvt2(x);
+  const f2 r1 = x - widen2(a);
+  b = cvt2(r1);
+  const f2 r2 = r1 - widen2(b);
+  c = cvt2(r2);
+}
+
+__device__ __forceinline__ f16v mma6(const bf8 (&a)[3], const bf8 (&b)[3], f16v acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
+// byte offset of 16-byte chunk ch (8 columns) of row `row` in a [BK][TN] bf16 image
+__device__ __forceinline__ uint32_t boff(int row, int ch) {
+  return (uint32_t)(256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))));
+}
+
+// A (M x K) = w (row-major, M x K, stride lda) or w^T (w: K x M row-major, stride lda) -> packed parts
+__global__ void __launch_bounds__(256) pack(const float* __restrict__ w, int64_t lda, int trans, int M, int K,
+                                            u4* __restrict__ out) {
+  const int KS = K / 16;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)(M / 32) * KS * 64) return;
+  const int lane = (int)(t & 63);
+  const int64_t g = t >> 6;  // mb * KS + ks
+  const int ks = (int)(g % KS), mb = (int)(g / KS);
+  const int m = 32 * mb + (lane & 31), k0 = 16 * ks + 8 * (lane >> 5);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = trans ? w[(int64_t)(k0 + j) * lda + m] : w[(int64_t)m * lda + k0 + j];
+  u4 p0, p1, p2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f2 x;
+    x.x = v[2 * i];
+    x.y = v[2 * i + 1];
+    uint32_t e0, e1, e2;
+    split2(x, e0, e1, e2);
+    p0[i] = e0, p1[i] = e1, p2[i] = e2;
+  }
+  out[(g * 3 + 0) * 64 + lane] = p0;
+  out[(g * 3 + 1) * 64 + lane] = p1;
+  out[(g * 3 + 2) * 64 + lane] = p2;
+}
+
+struct Args {
+  const u4* ap;  // packed A
+  const float* b0;
+  int64_t b0s;
+  const float* b1;
+  int64_t b1s;
+  float* c0;
+  int64_t c0s;
+  float* c1;
+  int64_t c1s;
+  const float* bias;  // (M) or null
+  int64_t ncols;      // nodes * P
+  int32_t M, K, k0, m0, P, mtiles;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+template <int WMW>
+__device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
+  using G = Geo<WMW>;
+  constexpr int TM = G::TM, NW = G::NW, A_PIECES = G::A_PIECES, A_BYTES = G::A_BYTES, BUF_BYTES = G::BUF_BYTES;
+  extern __shared__ u4 lds[];
+  char* ldsb = reinterpret_cast<char*>(lds);
+  // XCD-aware tile order: the m tiles of one column tile run on one XCD and share its L2 (B is read
+  // once from HBM per column tile)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int mt = id % a.mtiles, nt = id / a.mtiles;
+  const int64_t nbase = (int64_t)nt * TN;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int KS = a.K / 16, nst = a.K / BK, ks0 = a.k0 / BK, MB = a.M / 32;
+
+  // ---- A: LDS-DMA pieces pc = (mbl 2 + ksl) 3 + p (local m block, 16-k step, part), pc = w + NW i
+  const __amdgpu_buffer_rsrc_t ra = rsrc(a.ap);
+  uint32_t va[A_PIECES / NW];
+#pragma unroll
+  for (int i = 0; i < A_PIECES / NW; ++i) {
+    const int pc = w + NW * i;
+    const int mbl = pc / 6, kp = pc % 6;  // kp = 3 ksl + p
+    const int mb = min(mt * (TM / 32) + mbl, MB - 1);  // blocks past M: any valid data, never stored
+    va[i] = (uint32_t)((((int64_t)mb * KS * 3 + kp) * 64 + lane) * 16);
+  }
+  auto issue_a = [&](int s, int buf) {
+#pragma unroll
+    for (int i = 0; i < A_PIECES / NW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, lds + (buf * BUF_BYTES + (w + NW * i) * 1024) / 16, 16, va[i],
+                                               (uint32_t)s * 6 * 1024, 0, 0);
+  };
+
+  // ---- B: thread t loads the 16-byte pieces (row (t >> 5) + KR j, columns 4 (t & 31) ..) of a stage
+  const int fc = threadIdx.x & 31, kr = threadIdx.x >> 5;
+  int64_t col = nbase + 4 * fc;
+  if (col > a.ncols - 4) col = a.ncols - 4;  // columns past the end: any valid data, never stored
+  const int64_t node = col / a.P, pix = col - node * a.P;
+  const float* bp0 = a.b0 + node * a.b0s + pix + (int64_t)kr * a.P;
+  const float* bp1 = a.b1 + node * a.b1s + pix + (int64_t)kr * a.P;
+  f4 breg[G::BJ];
+  auto load_b = [&](int s) {
+    const float* p = s < ks0 ? bp0 + (int64_t)s * BK * a.P : bp1 + (int64_t)(s - ks0) * BK * a.P;
+#pragma unroll
+    for (int j = 0; j < G::BJ; ++j) breg[j] = *reinterpret_cast<const f4*>(p + (int64_t)G::KR * j * a.P);
+  };
+  auto store_b = [&](int buf) {  // split the registers' stage into the buffer's three part images
+    char* bimg = ldsb + buf * BUF_BYTES + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < G::BJ; ++j) {
+      u2 p0, p1, p2;
+      f2 lo, hi;
+      lo.x = breg[j].x, lo.y = breg[j].y, hi.x = breg[j].z, hi.y = breg[j].w;
+      uint32_t l0, l1, l2, h0, h1, h2;
+      split2(lo, l0, l1, l2);
+      split2(hi, h0, h1, h2);
+      p0.x = l0, p1.x = l1, p2.x = l2, p0.y = h0, p1.y = h1, p2.y = h2;
+      const uint32_t o = boff(kr + G::KR * j, fc >> 1) + 8 * (fc & 1);
+      *reinterpret_cast<u2*>(bimg + o) = p0;
+      *reinterpret_cast<u2*>(bimg + B_PART_BYTES + o) = p1;
+      *reinterpret_cast<u2*>(bimg + 2 * B_PART_BYTES + o) = p2;
+    }
+  };
+
+  // ---- fragment reads of one 16-k step: A by row pieces (ds_read_b128), B by ds_read_b64_tr_b16
+  const int g16 = lane >> 4, i16 = lane & 15, hh = lane >> 5;
+  // tr read: lane 4q + p of its 16-lane group reads row r0 + q, columns c0 + 4p .. (c0 = 16 (g16 & 1))
+  const int trq = i16 >> 2, trp = i16 & 3;
+  auto read_step = [&](int buf, int ksl, bf8 (&af)[2][3], bf8 (&bf)[2][3]) {
+    const char* base = ldsb + buf * BUF_BYTES;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int pc = ((2 * wm + mi) * 2 + ksl) * 3 + p;
+        af[mi][p] = __builtin_bit_cast(bf8, *reinterpret_cast<const u4*>(base + pc * 1024 + lane * 16));
+      }
+    const char* bimg = base + A_BYTES;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        s4 v[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int row = 16 * ksl + 8 * hh + 4 * t + trq;
+          const int ch = (64 * wn + 32 * ni + 16 * (g16 & 1)) / 8 + (trp >> 1);
+          const char* addr = bimg + p * B_PART_BYTES + boff(row, ch) + 8 * (trp & 1);
+          v[t] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s4*)(reinterpret_cast<uintptr_t>(addr)));
+        }
+        u4 u;
+        u.x = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[0], v[0], 0, 1));
+        u.y = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[0], v[0], 2, 3));
+        u.z = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[1], v[1], 0, 1));
+        u.w = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[1], v[1], 2, 3));
+        bf[ni][p] = __builtin_bit_cast(bf8, u);
+      }
+  };
+
+  f16v acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  issue_a(0, 0);
+  load_b(0);
+#pragma unroll 1
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    // stage s's B registers and A pieces (own) landed; its buffer was last read in stage s - 2
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_b(buf);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage s visible to every wave; every wave is past stage s - 1's reads
+    if (s + 1 < nst) {
+      issue_a(s + 1, buf ^ 1);
+      load_b(s + 1);
+    }
+#pragma unroll
+    for (int ksl = 0; ksl < 2; ++ksl) {
+      bf8 af[2][3], bf[2][3];
+      read_step(buf, ksl, af, bf);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = mma6(af[mi], bf[ni], acc[mi][ni]);
+    }
+  }
+
+  // ---- epilogue: accumulator register r of lane (column l & 31, half hh) is row (r & 3) + 8 (r >> 2) + 4 hh
+  const int mbase = mt * TM + 64 * wm;
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int64_t n = nbase + 64 * wn + 32 * ni + (lane & 31);
+    if (n >= a.ncols) continue;
+    const int64_t nd = n / a.P, px = n - nd * a.P;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mbase + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (m >= a.M) continue;
+        float v = acc[mi][ni][r];
+        if (a.bias != nullptr) v = __fadd_rn(v, a.bias[m]);
+        float* dst = m < a.m0 ? a.c0 + nd * a.c0s + (int64_t)m * a.P + px
+                              : a.c1 + nd * a.c1s + (int64_t)(m - a.m0) * a.P + px;
+        *dst = v;
+      }
+  }
+}
+
+__global__ void __launch_bounds__(256, 1) gemm_nn_split_w2(Args a) { gemm_nn_split_body<2>(a); }
+__global__ void __launch_bounds__(512, 1) gemm_nn_split_w4(Args a) { gemm_nn_split_body<4>(a); }
+
+constexpr int64_t kOffMax = (int64_t)1 << 31;
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <int WMW>
+hipError_t launch_w(Args a, hipStream_t st, const void* fn, void (*kern)(Args)) {
+  using G = Geo<WMW>;
+  a.mtiles = (a.M + G::TM - 1) / G::TM;
+  const int64_t grid = (int64_t)a.mtiles * ((a.ncols + TN - 1) / TN);
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  hipError_t attr = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch(Args a, hipStream_t st) {
+  if (a.K % BK != 0 || a.k0 % BK != 0 || a.M % 32 != 0 || a.P % 4 != 0) return hipErrorNotSupported;
+  if ((int64_t)a.M * a.K * 6 >= kOffMax) return hipErrorNotSupported;
+  // 256-row workgroups (8 waves, two per SIMD: one splits and stages while the other multiplies, and
+  // each B stage serves twice the rows) when M is a multiple of 256, else 128-row ones
+  const int v = mrp_host::tuning().gemm_split;
+  const bool wide = v == 4 || (v < 0 && a.M % 256 == 0);
+  return wide ? launch_w<4>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w4), gemm_nn_split_w4)
+              : launch_w<2>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w2), gemm_nn_split_w2);
+}
+
+}  // namespace mrp_cs
+
+using namespace mrp_cs;
+
+extern "C" int64_t mrp_compress_split_pack_bytes(int32_t M, int32_t K) {
+  if (M <= 0 || K <= 0 || M % 32 != 0 || K % 16 != 0) return 0;
+  return (int64_t)M * K * 6;
+}
+
+extern "C" int mrp_compress_split_pack(const float* w, int64_t ld, int32_t transpose, int32_t M, int32_t K,
+                                       void* packed, void* stream) {
+  if (M <= 0 || K <= 0 || ld <= 0) return hipErrorInvalidValue;
+  if (M % 32 != 0 || K % 16 != 0) return hipErrorNotSupported;
+  if (!w || !packed || !aligned16(packed)) return hipErrorInvalidValue;
+  const int64_t threads = (int64_t)(M / 32) * (K / 16) * 64;
+  hipLaunchKernelGGL(pack, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream), w,
+                     ld, transpose ? 1 : 0, M, K, static_cast<u4*>(packed));
+  return hipGetLastError();
+}
+
+extern "C" int mrp_compress_fwd_split(const float* x, int64_t x_node_stride, const float* agg, int64_t agg_node_stride,
+                                      int32_t num_nodes, int32_t C, int32_t P, const void* packed_w, const float* bias,
+                                      float* y, int64_t y_node_stride, void* stream) {
+  if (num_nodes < 0 || C < 0 || P < 0) return hipErrorInvalidValue;
+  if (num_nodes == 0 || C == 0 || P == 0) return hipSuccess;
+  const int64_t plane = (int64_t)C * P;
+  if (!x || !agg || !packed_w || !y || x_node_stride < plane || agg_node_stride < plane || y_node_stride < plane)
+    return hipErrorInvalidValue;
+  if (C % 32 != 0 || P % 4 != 0 || (x_node_stride & 3) || (agg_node_stride & 3) || !aligned16(x) || !aligned16(agg) ||
+      !aligned16(packed_w))
+    return hipErrorNotSupported;
+  Args a = {};
+  a.ap = static_cast<const u4*>(packed_w);
+  a.b0 = x;
+  a.b0s = x_node_stride;
+  a.b1 = agg;
+  a.b1s = agg_node_stride;
+  a.c0 = y;
+  a.c0s = y_node_stride;
+  a.c1 = y;
+  a.c1s = y_node_stride;
+  a.bias = bias;
+  a.ncols = (int64_t)num_nodes * P;
+  a.M = C;
+  a.K = 2 * C;
+  a.k0 = C;
+  a.m0 = C;
+  a.P = P;
+  return launch(a, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int mrp_compress_bwd_data_split(const float* gy, int64_t gy_node_stride, int32_t num_nodes, int32_t C,
+                                           int32_t P, const void* packed_wt, float* gx, int64_t gx_node_stride,
+                                           float* gagg, int64_t gagg_node_stride, void* stream) {
+  if (num_nodes < 0 || C < 0 || P < 0) return hipErrorInvalidValue;
+  if (num_nodes == 0 || C == 0 || P == 0) return hipSuccess;
+  const int64_t plane = (int64_t)C * P;
+  if (!gy || !packed_wt || !gx || !gagg || gy_node_stride < plane || gx_node_stride < plane ||
+      gagg_node_stride < plane)
+    return hipErrorInvalidValue;
+  if (C % 32 != 0 || P % 4 != 0 || (gy_node_stride & 3) || !aligned16(gy) || !aligned16(packed_wt))
+    return hipErrorNotSupported;
+  Args a = {};
+  a.ap = static_cast<const u4*>(packed_wt);
+  a.b0 = gy;
+  a.b0s = gy_node_stride;
+  a.b1 = gy;
+  a.b1s = gy_node_stride;
+  a.c0 = gx;
+  a.c0s = gx_node_stride;
+  a.c1 = gagg;
+  a.c1s = gagg_node_stride;
+  a.bias = nullptr;
+  a.ncols = (int64_t)num_nodes * P;
+  a.M = 2 * C;
+  a.K = C;
+  a.k0 = C;
+  a.m0 = C;
+  a.P = P;
+  return launch(a, static_cast<hipStream_t>(stream));
+}

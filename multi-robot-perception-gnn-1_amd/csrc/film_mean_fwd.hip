@@ -72,7 +72,7 @@ Tuning& tuning() {
 
 extern "C" {
 
-int mrp_abi_version(void) { return 14; }
+int mrp_abi_version(void) { return 15; }
 
 int mrp_tuning_set(const char* name, int32_t value) {
   if (name == nullptr) return hipErrorInvalidValue;
@@ -108,6 +108,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"edge_gemm", &t.edge_gemm, 0, 1},
       {"edge_fused", &t.edge_fused, 0, 4},
       {"edge_split_cb", &t.edge_split_cb, 1, 2},
+      {"gemm_split", &t.gemm_split, -1, 4},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {

@@ -141,7 +141,7 @@ class GCN(nn.Module):
         split-K weight-gradient kernel (``compress.FilmCompressFunction``).  With
         ``compress.set_compress_path('library')``: the cat kernel + torch's library GEMMs."""
         x = feats
-        if (x.is_cuda and self._return_mode() != "input" and compress_path() == "hip"
+        if (x.is_cuda and self._return_mode() != "input" and compress_path() != "library"
                 and film_compress_supported(conv, x)):
             mode = _opt(self.opt, "gcn_mode", "film_mean")
             if mode == "copy_mean":

@@ -126,6 +126,17 @@ def test_split_encoder_validation_without_launch():
     assert lib.mrp_edge_encoder_fwd_split(None, None, None, -1, 64, None, None) == HIP_INVALID_VALUE
 
 
+def test_split_compress_validation_without_launch():
+    lib = m.load_library()
+    assert lib.mrp_compress_split_pack_bytes(512, 1024) == 512 * 1024 * 6
+    assert lib.mrp_compress_split_pack_bytes(40, 64) == 0
+    assert lib.mrp_compress_split_pack(None, 64, 0, 40, 64, None, None) == m._lib.HIP_ERROR_NOT_SUPPORTED
+    assert lib.mrp_compress_split_pack(None, 64, 0, 64, 64, None, None) == HIP_INVALID_VALUE
+    assert lib.mrp_compress_fwd_split(None, 0, None, 0, 0, 64, 64, None, None, None, 0, None) == 0  # no nodes
+    assert lib.mrp_compress_fwd_split(None, 0, None, 0, 2, 64, 64, None, None, None, 0, None) == HIP_INVALID_VALUE
+    assert lib.mrp_compress_bwd_data_split(None, 0, 2, 64, 64, None, None, 0, None, 0, None) == HIP_INVALID_VALUE
+
+
 def test_tuning_knobs_documented_in_the_header():
     """mrp_tuning_set (host-only, no launch): every kernel-choice knob the header documents is accepted
     in range and rejected out of range; unknown names are rejected; "reset" restores defaults."""

@@ -1,10 +1,13 @@
-"""The matrix-core compress kernels (``csrc/compress_gemm.hip``: ``mrp_compress_fwd``,
-``mrp_compress_bwd_data``, ``mrp_compress_bwd_weight``) against a float64 restatement of the
+"""The matrix-core compress kernels — fp32 MFMA (``csrc/compress_gemm.hip``: ``mrp_compress_fwd``,
+``mrp_compress_bwd_data``, ``mrp_compress_bwd_weight``) and split-bf16 (``csrc/compress_split.hip``:
+``mrp_compress_fwd_split``, ``mrp_compress_bwd_data_split``) — against a float64 restatement of the
 reference's 1x1 conv over the concatenation (``dgl/model/models.py:163-165,182-184``).
 
 Bound: the error against float64 must be within max(1e-5, 4 x the error of torch's own fp32 GEMM of
 the same product) — i.e. as accurate as an fp32 computation of the reference op, whatever the
 summation order (``tests/stack_ref.within``)."""
+import contextlib
+
 import pytest
 import torch
 
@@ -26,6 +29,24 @@ def _ref(w, b, x, a, gy, dtype):
     return y, gcat[:, :C], gcat[:, C:], gw.reshape(C, 2 * C, 1, 1), g.sum((0, 2, 3))
 
 
+@contextlib.contextmanager
+def _path(path):
+    """"split" (per-shape workgroup), "split2" (128-row workgroups forced), "hip" (fp32 MFMA)."""
+    prev = m.compress.compress_path()
+    lib = m.load_library()
+    m.compress.set_compress_path("split" if path.startswith("split") else path)
+    if path == "split2":
+        assert lib.mrp_tuning_set(b"gemm_split", 2) == 0
+    try:
+        yield
+    finally:
+        m.compress.set_compress_path(prev)
+        lib.mrp_tuning_set(b"gemm_split", -1)
+
+
+PATHS = ["split", "split2", "hip"]
+
+
 def _check(ours, f32, f64, what):
     ok, errs = within(ours, f32, f64)
     assert ok, f"{what}: error {errs[0]:.3g} vs fp32 restatement {errs[1]:.3g}"
@@ -35,8 +56,9 @@ SHAPES = [(16, 64, 8, 8), (5, 96, 4, 4), (3, 32, 2, 2), (10, 128, 16, 16), (64, 
           (2, 32, 32, 32), (9, 224, 2, 6), (1, 32, 1, 4), (33, 96, 8, 8)]
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("n,C,H,W", SHAPES)
-def test_compress_gemm_matches_float64(cuda_device, n, C, H, W):
+def test_compress_gemm_matches_float64(cuda_device, n, C, H, W, path):
     torch.manual_seed(n * 131 + C)
     dev = cuda_device
     w = torch.randn(C, 2 * C, 1, 1, device=dev) / (2 * C) ** 0.5
@@ -44,9 +66,10 @@ def test_compress_gemm_matches_float64(cuda_device, n, C, H, W):
     x = torch.randn(n, C, H, W, device=dev)
     a = torch.randn(n, C, H, W, device=dev)
     gy = torch.randn(n, C, H, W, device=dev)
-    y = m.compress.compress_forward(w, b, x, a)
-    gx, ga = m.compress.compress_backward_data(w, gy)
-    r = m.compress.compress_backward_weight(gy, x, a)
+    with _path(path):
+        y = m.compress.compress_forward(w, b, x, a)
+        gx, ga = m.compress.compress_backward_data(w, gy)
+        r = m.compress.compress_backward_weight(gy, x, a)
     r64 = _ref(w, b, x, a, gy, torch.float64)
     r32 = _ref(w, b, x, a, gy, torch.float32)
     for name, o, f32, f64 in zip(("y", "gx", "ga"), (y, gx, ga), r32, r64):
@@ -77,7 +100,8 @@ def test_compress_function_declined_shapes(cuda_device, n, C, H, W):
         _check(o, f32, f64, name)
 
 
-def test_compress_gemm_cat_buffer_halves(cuda_device):
+@pytest.mark.parametrize("path", PATHS)
+def test_compress_gemm_cat_buffer_halves(cuda_device, path):
     """Operands and outputs as the two halves of (N, 2C, H, W) buffers (node stride 2 C P)."""
     torch.manual_seed(3)
     n, C, H, W = 12, 96, 8, 8
@@ -87,10 +111,11 @@ def test_compress_gemm_cat_buffer_halves(cuda_device):
     cat = torch.randn(n, 2 * C, H, W, device=dev)
     x, a = cat[:, :C], cat[:, C:]
     gy = torch.randn(n, C, H, W, device=dev)
-    y = m.compress.compress_forward(w, b, x, a)
     gcat = torch.full((n, 2 * C, H, W), float("nan"), device=dev)
-    m.compress.compress_backward_data(w, gy, gcat[:, :C], gcat[:, C:])
-    gw, gb = m.compress.compress_backward_weight(gy, x, a)
+    with _path(path):
+        y = m.compress.compress_forward(w, b, x, a)
+        m.compress.compress_backward_data(w, gy, gcat[:, :C], gcat[:, C:])
+        gw, gb = m.compress.compress_backward_weight(gy, x, a)
     r64 = _ref(w, b, x.contiguous(), a.contiguous(), gy, torch.float64)
     r32 = _ref(w, b, x.contiguous(), a.contiguous(), gy, torch.float32)
     _check(y, r32[0], r64[0], "y")
@@ -99,8 +124,9 @@ def test_compress_gemm_cat_buffer_halves(cuda_device):
     _check(gb, r32[4], r64[4], "gb")
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("n,C,H,W", [(128, 512, 32, 32), (256, 1280, 8, 8), (64, 2048, 8, 8), (128, 1024, 16, 16)])
-def test_compress_gemm_config_sizes(cuda_device, n, C, H, W):
+def test_compress_gemm_config_sizes(cuda_device, n, C, H, W, path):
     """The BASELINE configs' per-GPU layer shapes (configs[1..4]): forward, both gradients."""
     torch.manual_seed(C)
     dev = cuda_device
@@ -109,9 +135,10 @@ def test_compress_gemm_config_sizes(cuda_device, n, C, H, W):
     x = torch.randn(n, C, H, W, device=dev)
     a = torch.randn(n, C, H, W, device=dev)
     gy = torch.randn(n, C, H, W, device=dev)
-    y = m.compress.compress_forward(w, b, x, a)
-    gx, ga = m.compress.compress_backward_data(w, gy)
-    gw, gb = m.compress.compress_backward_weight(gy, x, a)
+    with _path(path):
+        y = m.compress.compress_forward(w, b, x, a)
+        gx, ga = m.compress.compress_backward_data(w, gy)
+        gw, gb = m.compress.compress_backward_weight(gy, x, a)
     r64 = _ref(w, b, x, a, gy, torch.float64)
     r32 = _ref(w, b, x, a, gy, torch.float32)
     del x, a
@@ -119,7 +146,8 @@ def test_compress_gemm_config_sizes(cuda_device, n, C, H, W):
         _check(o, f32, f64, name)
 
 
-def test_compress_gemm_deterministic(cuda_device):
+@pytest.mark.parametrize("path", PATHS)
+def test_compress_gemm_deterministic(cuda_device, path):
     torch.manual_seed(5)
     n, C, H, W = 64, 256, 8, 8
     dev = cuda_device
@@ -127,12 +155,41 @@ def test_compress_gemm_deterministic(cuda_device):
     a = torch.randn(n, C, H, W, device=dev)
     gy = torch.randn(n, C, H, W, device=dev)
     w = torch.randn(C, 2 * C, 1, 1, device=dev)
-    first = m.compress.compress_backward_weight(gy, x, a)
-    fy = m.compress.compress_forward(w, None, x, a)
-    for _ in range(3):
-        again = m.compress.compress_backward_weight(gy, x, a)
-        assert torch.equal(first[0], again[0]) and torch.equal(first[1], again[1])
-        assert torch.equal(fy, m.compress.compress_forward(w, None, x, a))
+    with _path(path):
+        first = m.compress.compress_backward_weight(gy, x, a)
+        fy = m.compress.compress_forward(w, None, x, a)
+        fd = m.compress.compress_backward_data(w, gy)
+        for _ in range(3):
+            again = m.compress.compress_backward_weight(gy, x, a)
+            assert torch.equal(first[0], again[0]) and torch.equal(first[1], again[1])
+            assert torch.equal(fy, m.compress.compress_forward(w, None, x, a))
+            d = m.compress.compress_backward_data(w, gy)
+            assert torch.equal(fd[0], d[0]) and torch.equal(fd[1], d[1])
+
+
+def test_split_pack_follows_weight_updates(cuda_device):
+    """The packed split-bf16 weight images are rebuilt after an in-place (optimizer-style) update and
+    after clear_packed_weights() for writes through .data; the ABI declines unsupported shapes."""
+    torch.manual_seed(9)
+    n, C, H, W = 8, 64, 8, 8
+    dev = cuda_device
+    w = torch.nn.Parameter(torch.randn(C, 2 * C, 1, 1, device=dev) / (2 * C) ** 0.5)
+    b = torch.randn(C, device=dev)
+    x, a, gy = (torch.randn(n, C, H, W, device=dev) for _ in range(3))
+    with _path("split"):
+        y0 = m.compress.compress_forward(w, b, x, a)
+        with torch.no_grad():
+            w.mul_(-2.0)
+        y1 = m.compress.compress_forward(w, b, x, a)
+        _check(y1, *(_ref(w.detach(), b, x, a, gy, t)[0] for t in (torch.float32, torch.float64)), "y after update")
+        w.data.mul_(0.5)
+        m.compress.clear_packed_weights()
+        g1 = m.compress.compress_backward_data(w, gy)
+        r32, r64 = (_ref(w.detach(), b, x, a, gy, t) for t in (torch.float32, torch.float64))
+        _check(g1[0], r32[1], r64[1], "gx after .data write")
+    assert not torch.equal(y0, y1)
+    lib = m.load_library()
+    assert lib.mrp_compress_split_pack_bytes(48, 96) == 0 and lib.mrp_compress_split_pack_bytes(64, 128) == 64 * 128 * 6
 
 
 def test_compress_gemm_empty_and_unsupported(cuda_device):
