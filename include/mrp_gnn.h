@@ -272,6 +272,18 @@ int mrp_compress_bwd_data_split(const float* gy, int64_t gy_node_stride, int32_t
                                 int64_t gagg_node_stride, void* stream);
 
 /*
+ * The compress weight gradient (mrp_compress_bwd_weight's products) on the split-bf16 matrix cores:
+ * both operands are activations, split in the kernel on their way into LDS; K = num_nodes P split over
+ * workgroups into partial tiles summed in a fixed order (deterministic).  Workspace: device buffer of
+ * mrp_compress_bwd_weight_split_workspace(num_nodes, C, P) bytes (0: none needed).  Requirements (else
+ * hipErrorNotSupported): C % 64 == 0, P % 32 == 0, 16-byte aligned operands, node strides % 4 == 0.
+ */
+int64_t mrp_compress_bwd_weight_split_workspace(int32_t num_nodes, int32_t C, int32_t P);
+int mrp_compress_bwd_weight_split(const float* gy, int64_t gy_node_stride, const float* x, int64_t x_node_stride,
+                                  const float* a, int64_t a_node_stride, int32_t num_nodes, int32_t C, int32_t P,
+                                  float* gw, float* gbias, void* workspace, int64_t workspace_bytes, void* stream);
+
+/*
  * First layer of the edge encoder, dgl/model/models.py:147-148:  h = relu(pose W1^T + b1).
  *   pose (num_edges, 9), w1 (C, 9) (nn.Linear weight layout), b1 (C) -> h (num_edges, C), fp32.
  * The second Linear is mrp_edge_logits_fwd and its Sigmoid is fused into the aggregation
@@ -369,7 +381,8 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * 2 = 128 rows / 4 waves, 4 = 256 rows / 8 waves). */
 int mrp_tuning_set(const char* name, int32_t value);
 
-/* Library identification: ABI version (incremented on signature changes; 15 = this header: v14 plus
+/* Library identification: ABI version (incremented on signature changes; 16 = this header: v15 plus
+ * the split-bf16 weight gradient (mrp_compress_bwd_weight_split + workspace); 15: v14 plus
  * the split-bf16 compress forward / data gradient and their weight packing (mrp_compress_split_*,
  * mrp_compress_fwd_split, mrp_compress_bwd_data_split); 14: v13 plus
  * the split-bf16 edge encoder forward and its weight packing (mrp_edge_encoder_pack_bytes /

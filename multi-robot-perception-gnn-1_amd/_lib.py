@@ -34,6 +34,8 @@ EXPORTED_SYMBOLS = (
     "mrp_compress_split_pack",
     "mrp_compress_fwd_split",
     "mrp_compress_bwd_data_split",
+    "mrp_compress_bwd_weight_split_workspace",
+    "mrp_compress_bwd_weight_split",
     "mrp_edge_hidden_fwd",
     "mrp_edge_logits_fwd",
     "mrp_edge_encoder_fwd",
@@ -47,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 15
+ABI_VERSION = 16
 MAX_NODES = 16
 
 HIP_ERROR_NOT_SUPPORTED = 801  # hipErrorNotSupported: a fused path declines this shape
@@ -120,6 +122,10 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_compress_fwd_split.restype = ctypes.c_int
     lib.mrp_compress_bwd_data_split.argtypes = [_P, _I64, _I32, _I32, _I32, _P, _P, _I64, _P, _I64, _P]
     lib.mrp_compress_bwd_data_split.restype = ctypes.c_int
+    lib.mrp_compress_bwd_weight_split_workspace.argtypes = [_I32, _I32, _I32]
+    lib.mrp_compress_bwd_weight_split_workspace.restype = ctypes.c_int64
+    lib.mrp_compress_bwd_weight_split.argtypes = lib.mrp_compress_bwd_weight.argtypes
+    lib.mrp_compress_bwd_weight_split.restype = ctypes.c_int
     lib.mrp_edge_hidden_fwd.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
     lib.mrp_edge_logits_fwd.argtypes = [_P, _I32, _I32, _P, _P, _P, _P]

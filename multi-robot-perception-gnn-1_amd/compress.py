@@ -11,10 +11,10 @@ Per node n a 1x1 convolution over NCHW is ``y[n] = W [x[n]; a[n]] + b`` with W (
 * weight grad:  ``dW = sum_n dy[n] [x[n]; a[n]]^T`` and ``db = sum dy`` in one split-K kernel with a
   fixed-order sum of its partial tiles (deterministic), no (N, C, 2C) temporary, no layout copies.
 
-Arithmetic (:func:`set_compress_path`): ``"split"`` (default) runs the forward and the data gradient on
-the bf16 matrix cores with every fp32 operand split exactly into three bf16 parts and six partial
-products per product (``mrp_compress_fwd_split`` / ``mrp_compress_bwd_data_split``, as accurate as an
-fp32 GEMM: the omitted terms are below 2^-25 of each product) and the weight gradient on the fp32 MFMA;
+Arithmetic (:func:`set_compress_path`): ``"split"`` (default) runs all three products on the bf16
+matrix cores with every fp32 operand split exactly into three bf16 parts and six partial products per
+product (``mrp_compress_fwd_split`` / ``_bwd_data_split`` / ``_bwd_weight_split``, as accurate as an
+fp32 GEMM: the omitted terms are below 2^-25 of each product; the weight gradient where C % 64 == 0);
 ``"hip"`` runs all three on the fp32 MFMA (``mrp_compress_fwd`` / ``_bwd_data`` / ``_bwd_weight``, exact
 fp32 products).  Both are checked against float64 (``tests/stack_ref``).  The split weight images are
 built once per weight version (:func:`packed_weight`).
@@ -188,14 +188,21 @@ def compress_backward_weight(gy: torch.Tensor, x: torch.Tensor, a: torch.Tensor,
     a, as_ = _node_major(a)
     dw = torch.empty((C, 2 * C, 1, 1), device=gy.device, dtype=torch.float32)
     db = torch.empty((C,), device=gy.device, dtype=torch.float32) if want_bias else None
-    nbytes = int(lib.mrp_compress_bwd_weight_workspace(n, C, H * W, max(gs, xs, as_)))
+    P = H * W
+    split = _PATH[0] == "split" and C % 64 == 0 and P % 32 == 0
+    if split:
+        nbytes = int(lib.mrp_compress_bwd_weight_split_workspace(n, C, P))
+        fn, name = lib.mrp_compress_bwd_weight_split, "mrp_compress_bwd_weight_split"
+    else:
+        nbytes = int(lib.mrp_compress_bwd_weight_workspace(n, C, P, max(gs, xs, as_)))
+        fn, name = lib.mrp_compress_bwd_weight, "mrp_compress_bwd_weight"
     ws = torch.empty((nbytes + 3) // 4, device=gy.device, dtype=torch.float32) if nbytes > 0 else None
     with torch.cuda.device(gy.device):
-        code = lib.mrp_compress_bwd_weight(_ptr(gy), gs, _ptr(x), xs, _ptr(a), as_, n, C, H * W, _ptr(dw), _ptr(db),
-                                           _ptr(ws), nbytes, _stream(gy.device))
+        code = fn(_ptr(gy), gs, _ptr(x), xs, _ptr(a), as_, n, C, P, _ptr(dw), _ptr(db), _ptr(ws), nbytes,
+                  _stream(gy.device))
     if code == _lib.HIP_ERROR_NOT_SUPPORTED:
         return None
-    _lib.check(code, "mrp_compress_bwd_weight")
+    _lib.check(code, name)
     return dw, db
 
 

@@ -326,6 +326,230 @@ hipError_t launch(Args a, hipStream_t st) {
               : launch_w<2>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w2), gemm_nn_split_w2);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Weight gradient  dW[m][n] = sum_k dy[m][k] S[n][k],  db[m] = sum_k dy[m][k],  k = (node, pixel):
+// both operands are k-contiguous rows (a channel's P pixels of one node), so no transposing read is
+// needed — each thread loads 16-byte row pieces of a stage (A = dy: TMW rows, B = [x; agg]: 128 rows,
+// 32 pixels of one node), splits them and stores the three bf16 parts as [row][32 k] 64-byte rows (the
+// row's four 16-byte chunks rotated by (row >> 2) & 3, so the fragment reads meet every bank once),
+// from which a lane's eight consecutive k are one ds_read_b128.  K = Nt P is split over workgroups
+// (whole stages, each within one node) into per-split partial tiles summed in a fixed order by
+// split_sum_nt (deterministic); db from the fp32 dy pieces as loaded, per split.
+// ------------------------------------------------------------------------------------------------
+struct NTArgs {
+  const float* g;  // dy (nodes, M, P), node stride gs
+  int64_t gs;
+  const float* s0;  // rows [0, n0) of B: x (nodes, n0, P)
+  int64_t s0s;
+  const float* s1;  // rows [n0, N): agg
+  int64_t s1s;
+  float* out;   // [split][M][N]
+  float* outb;  // [split][M] or null
+  int64_t ktot, kchunk;
+  int32_t M, N, n0, P, mtiles, ntiles;
+};
+
+template <int WMW>
+struct NTGeo {
+  static constexpr int TM = 64 * WMW, NW = 2 * WMW, THREADS = 64 * NW;
+  static constexpr int ROWB = BK * 2;                                  // bytes per [row][32 k] bf16 row
+  static constexpr int A_PART = TM * ROWB, B_PART = TN * ROWB;
+  static constexpr int BUF_BYTES = 3 * (A_PART + B_PART);
+  static constexpr int LDS_BYTES = 2 * BUF_BYTES;                      // 144 KiB at WMW 4
+  static constexpr int RPP = THREADS / 8;                              // rows per load pass (8 pieces a row)
+  static constexpr int AJ = TM / RPP, BJ = TN / RPP;                   // A / B pieces per thread per stage
+};
+
+__device__ __forceinline__ uint32_t rowoff(int row, int chunk) {  // [row][4 chunks of 16 B], rotated
+  return (uint32_t)(64 * row + 16 * (chunk ^ ((row >> 2) & 3)));
+}
+
+template <int WMW>
+__device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a) {
+  using G = NTGeo<WMW>;
+  extern __shared__ u4 lds[];
+  char* ldsb = reinterpret_cast<char*>(lds);
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int tiles = a.mtiles * a.ntiles;
+  const int split = id / tiles, tid = id - split * tiles;
+  const int mt = tid % a.mtiles, nt = tid / a.mtiles;
+  const int mbase = mt * G::TM, nbase = nt * TN;
+  const int64_t kbeg = (int64_t)split * a.kchunk;
+  const int64_t kend = kbeg + a.kchunk < a.ktot ? kbeg + a.kchunk : a.ktot;
+  const int nst = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+
+  // ---- loads: thread t -> piece (t & 7) (4 pixels) of rows (t >> 3) + RPP j
+  const int pc4 = threadIdx.x & 7, r0 = threadIdx.x >> 3;
+  int64_t aoff[G::AJ], boffs[G::BJ];  // row offsets within a node (elements), fixed
+  bool bhi[G::BJ];
+#pragma unroll
+  for (int j = 0; j < G::AJ; ++j) aoff[j] = (int64_t)min(mbase + r0 + G::RPP * j, a.M - 1) * a.P + 4 * pc4;
+#pragma unroll
+  for (int j = 0; j < G::BJ; ++j) {
+    const int n = min(nbase + r0 + G::RPP * j, a.N - 1);
+    bhi[j] = n >= a.n0;
+    boffs[j] = (int64_t)(bhi[j] ? n - a.n0 : n) * a.P + 4 * pc4;
+  }
+  f4 areg[G::AJ], breg[G::BJ];
+  float rsum[G::AJ];
+#pragma unroll
+  for (int j = 0; j < G::AJ; ++j) rsum[j] = 0.f;
+  auto load = [&](int s) {
+    const int64_t k = kbeg + (int64_t)s * BK;
+    const int64_t nd = k / a.P, px = k - nd * a.P;
+    const float* gp = a.g + nd * a.gs + px;
+    const float* xp = a.s0 + nd * a.s0s + px;
+    const float* ap = a.s1 + nd * a.s1s + px;
+#pragma unroll
+    for (int j = 0; j < G::AJ; ++j) areg[j] = *reinterpret_cast<const f4*>(gp + aoff[j]);
+#pragma unroll
+    for (int j = 0; j < G::BJ; ++j) breg[j] = *reinterpret_cast<const f4*>((bhi[j] ? ap : xp) + boffs[j]);
+  };
+  auto store = [&](int buf) {
+    char* base = ldsb + buf * G::BUF_BYTES;
+    auto put = [&](char* img, int part_bytes, int row, const f4& v) {
+      u2 p0, p1, p2;
+      f2 lo, hi;
+      lo.x = v.x, lo.y = v.y, hi.x = v.z, hi.y = v.w;
+      uint32_t l0, l1, l2, h0, h1, h2;
+      split2(lo, l0, l1, l2);
+      split2(hi, h0, h1, h2);
+      p0.x = l0, p1.x = l1, p2.x = l2, p0.y = h0, p1.y = h1, p2.y = h2;
+      const uint32_t o = rowoff(row, pc4 >> 1) + 8 * (pc4 & 1);
+      *reinterpret_cast<u2*>(img + o) = p0;
+      *reinterpret_cast<u2*>(img + part_bytes + o) = p1;
+      *reinterpret_cast<u2*>(img + 2 * part_bytes + o) = p2;
+    };
+#pragma unroll
+    for (int j = 0; j < G::AJ; ++j) {
+      rsum[j] += (areg[j].x + areg[j].y) + (areg[j].z + areg[j].w);
+      put(base, G::A_PART, r0 + G::RPP * j, areg[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < G::BJ; ++j) put(base + 3 * G::A_PART, G::B_PART, r0 + G::RPP * j, breg[j]);
+  };
+  // fragments of one 16-k step: lane (r, hh) reads k = 16 ksl + 8 hh .. + 7 of row r: chunk 2 ksl + hh
+  const int hh = lane >> 5, rl = lane & 31;
+  auto read_step = [&](int buf, int ksl, bf8 (&af)[2][3], bf8 (&bf)[2][3]) {
+    const char* base = ldsb + buf * G::BUF_BYTES;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int row = 64 * wm + 32 * mi + rl;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        af[mi][p] = __builtin_bit_cast(bf8, *reinterpret_cast<const u4*>(base + p * G::A_PART + rowoff(row, 2 * ksl + hh)));
+    }
+    const char* bb = base + 3 * G::A_PART;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int row = 64 * wn + 32 * ni + rl;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bf[ni][p] = __builtin_bit_cast(bf8, *reinterpret_cast<const u4*>(bb + p * G::B_PART + rowoff(row, 2 * ksl + hh)));
+    }
+  };
+
+  f16v acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  if (nst > 0) load(0);
+#pragma unroll 1
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store(buf);  // its buffer was last read in stage s - 2
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nst) load(s + 1);
+#pragma unroll
+    for (int ksl = 0; ksl < 2; ++ksl) {
+      bf8 af[2][3], bf[2][3];
+      read_step(buf, ksl, af, bf);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = mma6(af[mi], bf[ni], acc[mi][ni]);
+    }
+  }
+
+  float* out = a.out + (int64_t)split * a.M * a.N;
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int n = nbase + 64 * wn + 32 * ni + rl;
+    if (n >= a.N) continue;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mbase + 64 * wm + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (m < a.M) out[(int64_t)m * a.N + n] = acc[mi][ni][r];
+      }
+  }
+  if (a.outb != nullptr && nt == 0) {  // the column-tile-0 workgroups write the split's row sums
+#pragma unroll
+    for (int j = 0; j < G::AJ; ++j) {
+      float v = rsum[j];  // the 8 threads of a row are 8 consecutive lanes (t & 7)
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      const int m = mbase + r0 + G::RPP * j;
+      if (pc4 == 0 && m < a.M) a.outb[(int64_t)split * a.M + m] = v;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(512, 1) gemm_nt_split_w4(NTArgs a) { gemm_nt_split_body<4>(a); }
+
+// out = sum over the splits of part (fixed order), the same for the row sums
+__global__ void __launch_bounds__(256) split_sum_nt(const f4* __restrict__ part, int nsplit, int64_t n4,
+                                                    f4* __restrict__ out, const float* __restrict__ partb, int32_t M,
+                                                    float* __restrict__ outb) {
+  const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t e = tid; e < n4; e += stride) {
+    f4 v = part[e];
+    for (int s = 1; s < nsplit; ++s) v += part[(int64_t)s * n4 + e];
+    out[e] = v;
+  }
+  if (outb != nullptr)
+    for (int64_t m = tid; m < M; m += stride) {
+      float v = partb[m];
+      for (int s = 1; s < nsplit; ++s) v += partb[(int64_t)s * M + m];
+      outb[m] = v;
+    }
+}
+
+// Splits of K = Nt P (whole stages): the count minimising (rounds of one-per-CU workgroups) x
+// (stages per split) plus the partial-tile traffic of the final sum.
+int nt_splits(int64_t tiles, int64_t ktot, int64_t M, int64_t N, int64_t* kchunk) {
+  const int64_t stages = ktot / BK;
+  int best = 1;
+  double best_cost = 1e300;
+  for (int s = 1; s <= 256; ++s) {
+    const int64_t per = (stages + s - 1) / s;
+    if ((stages + per - 1) / per != s) continue;  // some split would be empty
+    const int64_t rounds = (tiles * s + 255) / 256;
+    // one stage of a 256 x 128 workgroup at ~190 TF/s-equivalent: ~0.09 us
+    const double cost = (double)rounds * per * 0.09 + (s > 1 ? (double)M * N * 4.0 * (s + 1) / 4.0e6 + 4.0 : 0.0);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = s;
+    }
+  }
+  *kchunk = ((stages + best - 1) / best) * BK;
+  return best;
+}
+
 }  // namespace mrp_cs
 
 using namespace mrp_cs;
@@ -406,4 +630,75 @@ extern "C" int mrp_compress_bwd_data_split(const float* gy, int64_t gy_node_stri
   a.m0 = C;
   a.P = P;
   return launch(a, static_cast<hipStream_t>(stream));
+}
+
+namespace {
+bool nt_split_ok(int32_t num_nodes, int32_t C, int32_t P) {
+  return num_nodes > 0 && C > 0 && C % 64 == 0 && P % BK == 0;
+}
+}  // namespace
+
+extern "C" int64_t mrp_compress_bwd_weight_split_workspace(int32_t num_nodes, int32_t C, int32_t P) {
+  if (!nt_split_ok(num_nodes, C, P)) return 0;
+  const int64_t M = C, N = 2 * (int64_t)C;
+  const int64_t tiles = ((M + NTGeo<4>::TM - 1) / NTGeo<4>::TM) * ((N + TN - 1) / TN);
+  int64_t kchunk;
+  const int ns = nt_splits(tiles, (int64_t)num_nodes * P, M, N, &kchunk);
+  return ns <= 1 ? 0 : ((int64_t)ns * M * N + (int64_t)ns * M) * 4;
+}
+
+extern "C" int mrp_compress_bwd_weight_split(const float* gy, int64_t gy_node_stride, const float* x,
+                                             int64_t x_node_stride, const float* agg, int64_t agg_node_stride,
+                                             int32_t num_nodes, int32_t C, int32_t P, float* gw, float* gbias,
+                                             void* workspace, int64_t workspace_bytes, void* stream) {
+  if (num_nodes < 0 || C < 0 || P < 0) return hipErrorInvalidValue;
+  if (C == 0) return hipSuccess;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t M = C, N = 2 * (int64_t)C;
+  if (gw == nullptr && gbias == nullptr) return hipSuccess;
+  if (num_nodes == 0 || P == 0) {  // empty sum
+    if (gw && hipMemsetAsync(gw, 0, M * N * 4, st) != hipSuccess) return hipErrorUnknown;
+    if (gbias && hipMemsetAsync(gbias, 0, M * 4, st) != hipSuccess) return hipErrorUnknown;
+    return hipSuccess;
+  }
+  const int64_t plane = (int64_t)C * P;
+  if (!gy || !x || !agg || !gw || gy_node_stride < plane || x_node_stride < plane || agg_node_stride < plane)
+    return hipErrorInvalidValue;
+  if (!nt_split_ok(num_nodes, C, P) || (gy_node_stride & 3) || (x_node_stride & 3) || (agg_node_stride & 3) ||
+      !aligned16(gy) || !aligned16(x) || !aligned16(agg) || !aligned16(gw))
+    return hipErrorNotSupported;
+  using G = NTGeo<4>;
+  NTArgs a = {};
+  a.mtiles = (int32_t)((M + G::TM - 1) / G::TM);
+  a.ntiles = (int32_t)((N + TN - 1) / TN);
+  a.ktot = (int64_t)num_nodes * P;
+  const int ns = nt_splits((int64_t)a.mtiles * a.ntiles, a.ktot, M, N, &a.kchunk);
+  const int64_t need = ns == 1 ? 0 : ((int64_t)ns * M * N + (int64_t)ns * M) * 4;
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need || !aligned16(workspace))) return hipErrorInvalidValue;
+  float* ws = static_cast<float*>(workspace);
+  a.g = gy;
+  a.gs = gy_node_stride;
+  a.s0 = x;
+  a.s0s = x_node_stride;
+  a.s1 = agg;
+  a.s1s = agg_node_stride;
+  a.out = ns == 1 ? gw : ws;
+  a.outb = gbias == nullptr ? nullptr : (ns == 1 ? gbias : ws + (int64_t)ns * M * N);
+  a.M = (int32_t)M;
+  a.N = (int32_t)N;
+  a.n0 = C;
+  a.P = P;
+  const int64_t grid = (int64_t)a.mtiles * a.ntiles * ns;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split_w4),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(gemm_nt_split_w4, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
+  e = hipGetLastError();
+  if (e != hipSuccess || ns == 1) return e;
+  const int64_t n4 = M * N / 4;
+  const int64_t blocks = (n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048;
+  hipLaunchKernelGGL(split_sum_nt, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<const f4*>(ws), ns, n4,
+                     reinterpret_cast<f4*>(gw), a.outb, (int32_t)M, gbias);
+  return hipGetLastError();
 }

@@ -72,7 +72,7 @@ Tuning& tuning() {
 
 extern "C" {
 
-int mrp_abi_version(void) { return 15; }
+int mrp_abi_version(void) { return 16; }
 
 int mrp_tuning_set(const char* name, int32_t value) {
   if (name == nullptr) return hipErrorInvalidValue;

@@ -135,6 +135,12 @@ def test_split_compress_validation_without_launch():
     assert lib.mrp_compress_fwd_split(None, 0, None, 0, 0, 64, 64, None, None, None, 0, None) == 0  # no nodes
     assert lib.mrp_compress_fwd_split(None, 0, None, 0, 2, 64, 64, None, None, None, 0, None) == HIP_INVALID_VALUE
     assert lib.mrp_compress_bwd_data_split(None, 0, 2, 64, 64, None, None, 0, None, 0, None) == HIP_INVALID_VALUE
+    assert lib.mrp_compress_bwd_weight_split_workspace(128, 512, 1024) > 0  # split over K
+    assert lib.mrp_compress_bwd_weight_split_workspace(128, 96, 1024) == 0  # C % 64: declined
+    assert lib.mrp_compress_bwd_weight_split(None, 0, None, 0, None, 0, 2, 96, 64, None, None, None, 0, None) == 0
+    # gw given (never dereferenced on the host) but the operands missing
+    assert lib.mrp_compress_bwd_weight_split(None, 0, None, 0, None, 0, 2, 96, 64, 16, None, None, 0, None) == \
+        HIP_INVALID_VALUE
 
 
 def test_tuning_knobs_documented_in_the_header():

@@ -42,10 +42,15 @@ for name, n, C, H in SHAPES:
         if ref is None:
             ref = cm._lib_forward(w.double(), b.double(), x.double(), a.double())
         err = float((y.double() - ref).abs().max() / ref.abs().max())
+        if path == "library":
+            wg = lambda: cm._lib_backward_weight(gy, x, a, True)
+        else:
+            wg = lambda: cm.compress_backward_weight(gy, x, a)
         tf = time_launches([f], args.iters, dev)
         td = time_launches([d], args.iters, dev)
+        tw = time_launches([wg], args.iters, dev) if path != "split2" else float("nan")
         row.append(f"{path}: fwd {tf * 1e6:7.1f} us {flop / tf / 1e12:5.1f} TF/s (err {err:.1e}) "
-                   f"dgrad {td * 1e6:7.1f} us {flop / td / 1e12:5.1f} TF/s")
+                   f"dgrad {td * 1e6:7.1f} us {flop / td / 1e12:5.1f} wgrad {tw * 1e6:7.1f} us {flop / tw / 1e12:5.1f}")
     cm.set_compress_path("split")
     lib.mrp_tuning_set(b"gemm_split", -1)
     print(" | ".join(row), flush=True)
