@@ -36,9 +36,16 @@ import torch
 from . import _lib
 
 _PATH = ["split"]
+# products the "split" path runs on the split-bf16 kernels (the rest on the fp32 MFMA): "fwd", "dgrad",
+# "wgrad" (set_compress_path(..., split_ops=...); for A/B and accuracy studies)
+_SPLIT_OPS = {"fwd", "dgrad", "wgrad"}
 
 
-def set_compress_path(path: str) -> None:
+def _split(op: str) -> bool:
+    return _PATH[0] == "split" and op in _SPLIT_OPS
+
+
+def set_compress_path(path: str, split_ops=None) -> None:
     """``"split"`` (default): forward and data gradient on the split-bf16 matrix cores
     (``compress_split.hip``, fp32-accurate), weight gradient on the fp32 MFMA; ``"hip"``: all three on
     the fp32 MFMA (``compress_gemm.hip``); ``"library"``: the cat kernel + torch's library GEMMs (the
@@ -46,6 +53,12 @@ def set_compress_path(path: str) -> None:
     if path not in ("split", "hip", "library"):
         raise ValueError("compress path must be 'split', 'hip' or 'library'")
     _PATH[0] = path
+    if split_ops is not None:
+        ops = set(split_ops)
+        if not ops <= {"fwd", "dgrad", "wgrad"}:
+            raise ValueError("split_ops: a subset of {'fwd', 'dgrad', 'wgrad'}")
+        _SPLIT_OPS.clear()
+        _SPLIT_OPS.update(ops)
 
 
 # packed split-bf16 images of a compress weight, per weight tensor: id -> (weakref, {"fwd" | "bwd":
@@ -140,7 +153,7 @@ def compress_forward(weight: torch.Tensor, bias, x: torch.Tensor, a: torch.Tenso
     y = torch.empty((n, C, H, W), device=x.device, dtype=torch.float32)
     lib = _lib.load_library()
     with torch.cuda.device(x.device):
-        if _PATH[0] == "split":
+        if _split("fwd"):
             img = packed_weight(weight, "fwd")
             _lib.check(lib.mrp_compress_fwd_split(_ptr(x), xs, _ptr(a), as_, n, C, H * W, _ptr(img), _ptr(b), _ptr(y),
                                                   C * H * W, _stream(x.device)), "mrp_compress_fwd_split")
@@ -164,7 +177,7 @@ def compress_backward_data(weight: torch.Tensor, gy: torch.Tensor, gx: torch.Ten
         raise ValueError("compress_backward_data: outputs must be node-major fp32, 16-byte aligned")
     st = _stream(gy.device)
     with torch.cuda.device(gy.device):
-        if _PATH[0] == "split":
+        if _split("dgrad"):
             img = packed_weight(weight, "bwd")
             _lib.check(lib.mrp_compress_bwd_data_split(_ptr(gy), gs, n, C, H * W, _ptr(img), _ptr(gx), gxs, _ptr(ga),
                                                        gas, st), "mrp_compress_bwd_data_split")
@@ -189,7 +202,7 @@ def compress_backward_weight(gy: torch.Tensor, x: torch.Tensor, a: torch.Tensor,
     dw = torch.empty((C, 2 * C, 1, 1), device=gy.device, dtype=torch.float32)
     db = torch.empty((C,), device=gy.device, dtype=torch.float32) if want_bias else None
     P = H * W
-    split = _PATH[0] == "split" and C % 64 == 0 and P % 32 == 0
+    split = _split("wgrad") and C % 64 == 0 and P % 32 == 0
     if split:
         nbytes = int(lib.mrp_compress_bwd_weight_split_workspace(n, C, P))
         fn, name = lib.mrp_compress_bwd_weight_split, "mrp_compress_bwd_weight_split"

@@ -77,14 +77,22 @@ __device__ __forceinline__ void split2(f2 x, uint32_t& a, uint32_t& b, uint32_t&
   c = cvt2(r2);
 }
 
-__device__ __forceinline__ f16v mma6(const bf8 (&a)[3], const bf8 (&b)[3], f16v acc) {
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
-  return acc;
+// The six partial products of one 16-k step into two accumulators: the five small ones (at most 2^-8
+// of the product) into `lo`, a0 b0 into `hi`, summed once in the epilogue.  The bf16 MFMA rounds its
+// sum into the accumulator to nearest, but where the accumulator is large against the products the
+// low-order bits it drops are biased (tools/exp_split_dgrad.py: pixel sums of the data gradient 6x
+// the fp32 GEMM's error with one accumulator); with a0 b0 alone in `hi` the long accumulator sees a
+// sixth of the additions and the others happen 2^8 lower, and the bias falls to the fp32 GEMM's level.
+struct Acc2 {
+  f16v hi, lo;
+};
+__device__ __forceinline__ void mma6(const bf8 (&a)[3], const bf8 (&b)[3], Acc2& acc) {
+  acc.lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc.lo, 0, 0, 0);
+  acc.hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc.hi, 0, 0, 0);
 }
 
 // byte offset of 16-byte chunk ch (8 columns) of row `row` in a [BK][TN] bf16 image
@@ -241,13 +249,13 @@ __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
       }
   };
 
-  f16v acc[2][2];
+  Acc2 acc[2][2];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[mi][ni].hi[r] = acc[mi][ni].lo[r] = 0.f;
 
   issue_a(0, 0);
   load_b(0);
@@ -270,7 +278,7 @@ __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = mma6(af[mi], bf[ni], acc[mi][ni]);
+        for (int ni = 0; ni < 2; ++ni) mma6(af[mi], bf[ni], acc[mi][ni]);
     }
   }
 
@@ -287,7 +295,7 @@ __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
       for (int r = 0; r < 16; ++r) {
         const int m = mbase + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * hh;
         if (m >= a.M) continue;
-        float v = acc[mi][ni][r];
+        float v = __fadd_rn(acc[mi][ni].hi[r], acc[mi][ni].lo[r]);
         if (a.bias != nullptr) v = __fadd_rn(v, a.bias[m]);
         float* dst = m < a.m0 ? a.c0 + nd * a.c0s + (int64_t)m * a.P + px
                               : a.c1 + nd * a.c1s + (int64_t)(m - a.m0) * a.P + px;
@@ -454,13 +462,13 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a) {
     }
   };
 
-  f16v acc[2][2];
+  Acc2 acc[2][2];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[mi][ni].hi[r] = acc[mi][ni].lo[r] = 0.f;
 
   if (nst > 0) load(0);
 #pragma unroll 1
@@ -478,7 +486,7 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = mma6(af[mi], bf[ni], acc[mi][ni]);
+        for (int ni = 0; ni < 2; ++ni) mma6(af[mi], bf[ni], acc[mi][ni]);
     }
   }
 
@@ -492,7 +500,7 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = mbase + 64 * wm + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (m < a.M) out[(int64_t)m * a.N + n] = acc[mi][ni][r];
+        if (m < a.M) out[(int64_t)m * a.N + n] = __fadd_rn(acc[mi][ni].hi[r], acc[mi][ni].lo[r]);
       }
   }
   if (a.outb != nullptr && nt == 0) {  // the column-tile-0 workgroups write the split's row sums
