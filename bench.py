@@ -385,7 +385,7 @@ def config_record(cid, world, rank, device, args):
     rec = {"config": cfg["name"], "graphs_per_rank": hi - lo, "share": share, "robots": N, "channels": C,
            "H": H, "W": H, "layers": layers, "graph": f"k-NN({knn})" if knn else "complete",
            "graph_kind": "regular" if knn else "complete", "scaling": scaling}
-    # forward and training step on the matrix-core compress kernels ("hip", the product path) and, for
+    # forward and training step on the matrix-core compress kernels (the product path) and, for
     # comparison, on the cat kernel + torch's library GEMMs ("library", the round-2 path): timed
     # alternately, three rounds each, median per path — the first timed block of a sequence runs a
     # few % slow (clocks), which a single A-then-B comparison would credit to the path
