@@ -46,8 +46,10 @@ def _split(op: str) -> bool:
 
 
 def set_compress_path(path: str, split_ops=None) -> None:
-    """``"split"`` (default): forward and data gradient on the split-bf16 matrix cores
-    (``compress_split.hip``, fp32-accurate), weight gradient on the fp32 MFMA; ``"hip"``: all three on
+    """``"split"`` (default): forward, data gradient and weight gradient on the split-bf16 matrix
+    cores (``compress_split.hip``, fp32-accurate; the weight gradient falls back to the fp32 MFMA
+    where C % 64 or H W % 32 is not 0); ``split_ops`` narrows which of "fwd" / "dgrad" / "wgrad" take
+    the split kernels; ``"hip"``: all three on
     the fp32 MFMA (``compress_gemm.hip``); ``"library"``: the cat kernel + torch's library GEMMs (the
     round-2 path), for A/B measurement."""
     if path not in ("split", "hip", "library"):
