@@ -192,6 +192,9 @@ struct Tile {
   // the 4-8-way LDS bank conflicts an unpadded 64- or 256-float stride gives (rocprof r02: 70 % of
   // LDS cycles were conflicts at 8x8)
   static constexpr int SZ = NT * NTP + 4;
+  // row stride of the backward's per-channel sums S[v] (16-byte rows: written as vectors): 12 floats
+  // at N = 8 puts the 8 channels a half-wave reads in the epilogue (complete_epi_slot) on 8 banks
+  static constexpr int SLS = NTP + 4;
 };
 
 // Edge id of u -> v (u != v) in a complete graph of n nodes whose edges start at ebase and are
@@ -301,13 +304,63 @@ __device__ __forceinline__ void build_tiles_csr(const AggArgs& a, int node0, int
 //   complete_store : registers -> LDS (FWD layout [v][u] gamma and beta; BWD layout [u][v]
 //                    scaled gamma)
 // ---------------------------------------------------------------------------
+// Slot t of a COMPLETE prologue -> (channel cl, destination v, source u), channel fastest
+// (neighbouring lanes read neighbouring gamma/beta pairs): slot = t / cpb in [v][u] order.  With
+// 16-channel workgroups (the 8x8 planes) a 32-lane half of a wave holds 16 channels x 2 slots, and a
+// 68-float tile stride puts channels c and c + 8 on the same dword bank (mod 32, the ds_write_b32
+// banking), so there (a) TR: consecutive slots step v, i.e. along a row of the backward's
+// transposed [u][v] tiles (the forward's [v][u] tiles: u), and (b) within each aligned group of 4
+// slots channels 8-15 take the other two slots than channels 0-7 (slot ^ 2) — every half-wave's
+// stores then cover 32 banks (rocprof r03: 9 % of the forward's and 22 % of the backward's LDS
+// cycles were conflicts at 8x8 planes without it).
+template <int NT, bool TR>
+__device__ __forceinline__ void complete_slot(const AggArgs& a, int t, int& cl, int& v, int& u) {
+  int slot;
+  split_channel(a, t, cl, slot);
+  if ((NT * NT) % 4 == 0 && a.cpb == 16) {
+    slot ^= (cl & 8) >> 2;
+    const int hi = slot / NT, lo = slot - hi * NT;
+    v = TR ? lo : hi;
+    u = TR ? hi : lo;
+  } else {
+    v = slot / NT;
+    u = slot - v * NT;
+  }
+}
+
+// The backward epilogue's slot order.  16-channel workgroups: bits 3 and 5 of t swapped, so a
+// 32-lane half holds 8 channels x 4 consecutive slots (one destination v) and its reads of the Gram
+// [v][u], of S[v] (SLS) and of the per-slot sigmoid values (sg_index) each cover distinct banks;
+// other channel counts: the prologue's order.
+template <int NT>
+__device__ __forceinline__ void complete_epi_slot(const AggArgs& a, int t, int& cl, int& v, int& u) {
+  if ((NT * NT) % 4 == 0 && a.cpb == 16) {
+    const int ts = (t & ~0x28) | ((t & 8) << 2) | ((t & 32) >> 2);
+    cl = ts & 15;
+    const int slot = ts >> 4;
+    v = slot / NT;
+    u = slot - v * NT;
+  } else {
+    complete_slot<NT, true>(a, t, cl, v, u);
+  }
+}
+// Index of slot (cl, v, u) in the backward's per-slot sigmoid buffer.  16 channels: slot-major with
+// the channel XORed with 8 on every other pair of sources, so both the prologue's 16-lane stores (one
+// slot, 16 channels) and the epilogue's 32-lane reads (8 channels x 4 sources) are conflict-free;
+// otherwise the prologue's t.
+template <int NT>
+__device__ __forceinline__ int sg_index(const AggArgs& a, int cl, int v, int u) {
+  const int slot = v * NT + u;
+  return slot * a.cpb + (((NT * NT) % 4 == 0 && a.cpb == 16) ? cl ^ (((slot >> 1) & 1) << 3) : cl);
+}
+
 template <int NT>
 struct CompleteSlots {
   static constexpr int kSlots = NT * NT;
   static constexpr int kPer = (kMaxChanPerBlock * kSlots + kBlock - 1) / kBlock;  // max slots per thread
 };
 
-template <int NT>
+template <int NT, bool TR>
 __device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, int c0, int base, float2* reg) {
   constexpr int S = CompleteSlots<NT>::kSlots;
   const int tot = a.cpb * S;
@@ -316,9 +369,8 @@ __device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, 
     const int t = base + threadIdx.x + r * blockDim.x;
     float2 val = make_float2(0.f, 0.f);
     if (t < tot) {
-      int cl, slot;  // channel fastest -> neighbouring lanes read neighbouring pairs
-      split_channel(a, t, cl, slot);
-      const int v = slot / NT, u = slot - v * NT;
+      int cl, v, u;
+      complete_slot<NT, TR>(a, t, cl, v, u);
       const int c = c0 + cl;
       if (u != v && c < a.C) {
         if (a.mode == MRP_AGG_COPY_MEAN) {
@@ -348,15 +400,15 @@ __device__ __forceinline__ void complete_store(const AggArgs& a, int base, const
   for (int r = 0; r < CompleteSlots<NT>::kPer; ++r) {
     const int t = base + threadIdx.x + r * blockDim.x;
     if (t < tot) {
-      int cl, slot;
-      split_channel(a, t, cl, slot);
-      const int v = slot / NT, u = slot - v * NT;
+      int cl, v, u;
+      complete_slot<NT, BWD>(a, t, cl, v, u);
       float2 w = reg[r];
       // (diagonal and out-of-range slots hold 0 and turn into 0.5 here: never read)
       if (act) w = make_float2(sigmoidf(w.x), sigmoidf(w.y));
       if (BWD) {
         Ga[cl * SZ + u * NTP + v] = s * w.x;
-        if (Sg != nullptr) Sg[t] = w;  // sigmoid(z) of slot (cl, v, u), reused by the epilogue
+        // sigmoid(z) of slot (cl, v, u), reused by the epilogue (slot-major: its lane order differs)
+        if (Sg != nullptr) Sg[sg_index<NT>(a, cl, v, u)] = w;
       } else {
         Ga[cl * SZ + v * NTP + u] = w.x;
         Gb[cl * SZ + v * NTP + u] = w.y;
@@ -372,7 +424,7 @@ __device__ __forceinline__ void complete_rest(const AggArgs& a, int64_t ebase, i
   const int chunk = CompleteSlots<NT>::kPer * blockDim.x;
   for (int base = chunk; base < a.cpb * CompleteSlots<NT>::kSlots; base += chunk) {
     float2 reg[CompleteSlots<NT>::kPer];
-    complete_fetch<NT>(a, ebase, c0, base, reg);
+    complete_fetch<NT, BWD>(a, ebase, c0, base, reg);
     complete_store<NT, BWD>(a, base, reg, Ga, Gb, Sg);
   }
 }
@@ -424,7 +476,7 @@ __global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   // prologue part 1 (COMPLETE): gamma/beta into registers
   float2 reg[CompleteSlots<NT>::kPer];
   const int64_t ebase = (int64_t)b * NT * (NT - 1);
-  if (COMPLETE) complete_fetch<NT>(a, ebase, c0, 0, reg);
+  if (COMPLETE) complete_fetch<NT, false>(a, ebase, c0, 0, reg);
   // first slice of the sweep, issued before the weight tiles are needed
   int j = jbeg + li;
   // element k of every source's slice in one NT-wide vector value: when the compiler keeps a
@@ -803,7 +855,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_dx(AggArgs a) {
 
   if (COMPLETE) {
     float2 reg[CompleteSlots<NT>::kPer];
-    complete_fetch<NT>(a, (int64_t)b * NT * (NT - 1), c0, 0, reg);
+    complete_fetch<NT, true>(a, (int64_t)b * NT * (NT - 1), c0, 0, reg);
     complete_store<NT, true>(a, 0, reg, Wt, nullptr);
     complete_rest<NT, true>(a, (int64_t)b * NT * (NT - 1), c0, Wt, nullptr);
   } else {
@@ -926,11 +978,12 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   // wave reduces its own Gram partial and the epilogue adds the wpc partials in wave order
   const int wpc = a.lpc > 64 ? a.lpc >> 6 : 1;
   const int npg = a.cpb * wpc;   // Gram partials
+  constexpr int SLS = Tile<NT>::SLS;
   float* Wt = smem;              // [cpb][NT][NTP]   scaled, transposed
   float* Dl = Wt + a.cpb * SZ;   // [npg][NT][NTP]   Gram (unscaled)
-  float* Sl = Dl + npg * SZ;     // [npg][NTP]       sum_p G_v
-  float* sc = Sl + npg * NTP;    // [NTP]            s_v
-  // COMPLETE with logits: sigmoid(z) of every slot, (cpb x NT x NT) float2 in complete_fetch order,
+  float* Sl = Dl + npg * SZ;     // [npg][SLS]       sum_p G_v
+  float* sc = Sl + npg * SLS;    // [NTP]            s_v
+  // COMPLETE with logits: sigmoid(z) of every slot, (NT x NT x cpb) float2, slot-major,
   // so the epilogue's sigmoid backward does not fetch z from HBM a second time
   float2* Sg = (COMPLETE && a.logits) ? reinterpret_cast<float2*>(sc + NTP) : nullptr;
 
@@ -979,7 +1032,7 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
   auto load_slice = [&](int vb, int j) { load_into(gv, xv, vb, j); };
 
   float2 reg[CompleteSlots<NT>::kPer];
-  if (COMPLETE) complete_fetch<NT>(a, (int64_t)b * NT * (NT - 1), c0, 0, reg);
+  if (COMPLETE) complete_fetch<NT, true>(a, (int64_t)b * NT * (NT - 1), c0, 0, reg);
   if (kOnePass && active && li < a.PV) load_slice(0, li);
   if (PRE2 && active && li < a.PV) load_into(gv2, xv2, 0, li + a.lpc);
   if (COMPLETE) {
@@ -1085,7 +1138,7 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
         for (int i = 0; i < VB; ++i) {
           const int v = vb + i;
           if (v < NT) {
-            Sl[pg * NTP + v] = S[i];
+            Sl[pg * SLS + v] = S[i];
 #pragma unroll
             for (int u = 0; u < NT; ++u) Dl[pg * SZ + v * NTP + u] = D[i][u];
           }
@@ -1100,21 +1153,20 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
     const float s = ((a.mode != MRP_AGG_FILM_SUM && NT > 1) ? 1.f / (float)(NT - 1) : 1.f) * a.agg_scale;
     const int64_t ebase = (int64_t)b * NT * (NT - 1);
     for (int t = threadIdx.x; t < a.cpb * NT * NT; t += blockDim.x) {
-      int cl, slot;
-      split_channel(a, t, cl, slot);
-      const int v = slot / NT, u = slot - v * NT;
+      int cl, v, u;
+      complete_epi_slot<NT>(a, t, cl, v, u);
       const int cc = c0 + cl;
       if (u == v || cc >= a.C) continue;
-      float dd = Dl[cl * wpc * SZ + v * NTP + u], ss = Sl[cl * wpc * NTP + v];
+      float dd = Dl[cl * wpc * SZ + v * NTP + u], ss = Sl[cl * wpc * SLS + v];
       for (int w = 1; w < wpc; ++w) {
         dd += Dl[(cl * wpc + w) * SZ + v * NTP + u];
-        ss += Sl[(cl * wpc + w) * NTP + v];
+        ss += Sl[(cl * wpc + w) * SLS + v];
       }
       float2 r = make_float2(s * dd, s * ss);
       const int64_t off = (complete_eid(ebase, NT, u, v) * a.C + cc) * 2;
       if (a.logits) {
         // d z = d(gamma, beta) * sig * (1 - sig), sig = sigmoid(z) kept from the prologue
-        const float2 sg = Sg[t];
+        const float2 sg = Sg[sg_index<NT>(a, cl, v, u)];
         r = make_float2(r.x * sg.x * (1.f - sg.x), r.y * sg.y * (1.f - sg.y));
       }
       *reinterpret_cast<float2*>(a.dgb + off) = r;
@@ -1132,8 +1184,8 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
     const int beg = a.indptr[node0 + v];
     const int end = a.indptr[node0 + v + 1];
     const float s = sc[v];
-    float ss = Sl[cl * wpc * NTP + v];
-    for (int w = 1; w < wpc; ++w) ss += Sl[(cl * wpc + w) * NTP + v];
+    float ss = Sl[cl * wpc * SLS + v];
+    for (int w = 1; w < wpc; ++w) ss += Sl[(cl * wpc + w) * SLS + v];
     const float dbeta = s * ss;
     for (int k = beg; k < end; ++k) {
       const int u = a.src[k] - node0;
@@ -1440,13 +1492,20 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
   constexpr int CPB = 4 * CPW * CB;        // channels per workgroup
   constexpr int NS = NPB * KMAX;           // REGULAR edge slots
   constexpr int WR = NPB + 1;              // per-channel Wt / D row stride (floats)
-  constexpr int TR = 32 + 4;               // transpose tile row stride: 32 pixels + 4 (rows 4 banks apart)
+  // per-channel Wt / D stride: the prologue's 32-lane stores (CPB channels x 32 / CPB destinations)
+  // land on 32 different banks (NPB = 16: 8 channels 20 banks apart mod 32; unpadded, 272 = 16 mod 32
+  // was 4-way, rocprof r03: 24 % of the k-NN backward's LDS cycles)
+  constexpr int CS = NPB * WR + (NPB == 16 ? 4 : 2);
+  constexpr int SS = NPB + 1;              // per-channel S stride: odd, the epilogue's 8-16 channels on distinct banks
+  // transpose tile row stride: 32 pixels + 8, so the 16-lane groups of the by-node ds_read_b128
+  // (rows jl, column chunk q) cover distinct banks (+4 was 2-way)
+  constexpr int TR = 32 + 8;
   extern __shared__ float4 smem_f4[];
   float* smem = reinterpret_cast<float*>(smem_f4);
-  float* Wt = smem;                   // [CPB][NPB][WR]  Wt[u][v]; each channel's rows become D[v][u]
-  float* Tt = Wt + CPB * NPB * WR;    // [4][16][TR]     per-wave transpose tile (half a pixel group)
-  float* Sl = Tt + 4 * 16 * TR;       // [CPB][NPB]
-  int* slot_u = reinterpret_cast<int*>(Sl + CPB * NPB);  // [NS] (REGULAR)
+  float* Wt = smem;                   // [CPB][CS]       Wt[u][v] (rows of WR); each channel's rows become D[v][u]
+  float* Tt = Wt + CPB * CS;          // [4][16][TR]     per-wave transpose tile (half a pixel group)
+  float* Sl = Tt + 4 * 16 * TR;       // [CPB][SS]
+  int* slot_u = reinterpret_cast<int*>(Sl + CPB * SS);  // [NS] (REGULAR)
   int* slot_e = slot_u + NS;                              // [NS]
 
   const int b = blockIdx.x / a.ncb;
@@ -1564,7 +1623,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
         for (int jj = 0; jj < NE; ++jj)  // += in slot order: multi-edges sum like the CSR tile build
           if (us[jj] == u) wv += s * gm[jj];
       }
-      Wt[(pcl * NPB + u) * WR + pv] = wv;
+      Wt[pcl * CS + u * WR + pv] = wv;
     }
     if (!COMPLETE && pcl == 0) {
 #pragma unroll
@@ -1592,7 +1651,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
 #pragma unroll
       for (int bb = 0; bb < 4; ++bb) {
         const int vn = 4 * q + bb;
-        wa[bb] = (jl / NPB == vn / NPB) ? Wt[((cbl + jl / NPB) * NPB + jl % NPB) * WR + vn % NPB] : 0.f;
+        wa[bb] = (jl / NPB == vn / NPB) ? Wt[(cbl + jl / NPB) * CS + (jl % NPB) * WR + vn % NPB] : 0.f;
       }
       dacc = mf4{0.f, 0.f, 0.f, 0.f};
       sacc = 0.f;
@@ -1651,9 +1710,9 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int vn = 4 * q + r;
-          if (vn / NPB == jl / NPB) Wt[((cbl + vn / NPB) * NPB + vn % NPB) * WR + jl % NPB] = dacc[r];
+          if (vn / NPB == jl / NPB) Wt[(cbl + vn / NPB) * CS + (vn % NPB) * WR + jl % NPB] = dacc[r];
         }
-        if (q == 0) Sl[(cbl + hx) * NPB + nx] = sacc;
+        if (q == 0) Sl[(cbl + hx) * SS + nx] = sacc;
       }
     }
   };
@@ -1690,7 +1749,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
       if (e < 0) continue;
     }
     const int64_t off = (e * a.C + cc) * 2;
-    float2 r = make_float2(s * Wt[(cl * NPB + v) * WR + u], s * Sl[cl * NPB + v]);
+    float2 r = make_float2(s * Wt[cl * CS + v * WR + u], s * Sl[cl * SS + v]);
     if (a.logits) r = sigmoid_backward(r, *reinterpret_cast<const float2*>(a.gb + off));
     *reinterpret_cast<float2*>(a.dgb + off) = r;
   }
@@ -1759,14 +1818,15 @@ size_t lds_regular(int cpb) {
 }
 // film_bwd_mfma: Wt/D + transpose tiles + S + slot table (cpb channels of npb nodes)
 inline size_t lds_mfma(int cpb, int npb, int kmax) {
-  return (size_t)(cpb * npb * (npb + 1) + 4 * 16 * 36 + cpb * npb) * sizeof(float) + 2 * (size_t)npb * kmax * sizeof(int);
+  const int cs = npb * (npb + 1) + (npb == 16 ? 4 : 2);  // film_bwd_mfma's CS, TR, SS
+  return (size_t)(cpb * cs + 4 * 16 * 40 + cpb * (npb + 1)) * sizeof(float) + 2 * (size_t)npb * kmax * sizeof(int);
 }
 template <int NT>
 size_t lds_bwd(int cpb, bool complete_logits, int lpc = 64) {
   // + the per-slot sigmoid values (float2) the COMPLETE epilogue reuses; one Gram partial per channel
   // group, or per wave when a plane spans several waves (lpc > 64)
   const int npg = lpc > 64 ? cpb * (lpc >> 6) : cpb;
-  return (size_t)(cpb * mrp::Tile<NT>::SZ + npg * mrp::Tile<NT>::SZ + npg * mrp::Tile<NT>::NTP +
+  return (size_t)(cpb * mrp::Tile<NT>::SZ + npg * mrp::Tile<NT>::SZ + npg * mrp::Tile<NT>::SLS +
                   mrp::Tile<NT>::NTP) * sizeof(float) +
          (complete_logits ? (size_t)cpb * NT * NT * sizeof(float2) : 0);
 }
