@@ -377,7 +377,8 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * kernel variants "gemm_nn" / "gemm_nt" (-1, default: the per-shape choice; 0..5: compress_gemm.hip's
  * variant table); "edge_gemm" (1, default: mrp_edge_logits_fwd on 32x32x2 MFMAs; 0: 16x16x4); "edge_fused"
  * (mrp_edge_encoder_fwd tile/buffer variant, 0..4); "edge_split_cb" (mrp_edge_encoder_fwd_split: 32-column
- * blocks per wave, 1 or 2 (default)); "gemm_split" (split-bf16 compress GEMM workgroup: -1 per shape,
+ * blocks per wave, 1 or 2; 0, default: per shape); "edge_split_k" (its hidden blocks over 1 or 2
+ * wave sets, 2 only when C % 64 == 0; 0, default: per shape); "gemm_split" (split-bf16 compress GEMM workgroup: -1 per shape,
  * 2 = 128 rows / 4 waves, 4 = 256 rows / 8 waves). */
 int mrp_tuning_set(const char* name, int32_t value);
 

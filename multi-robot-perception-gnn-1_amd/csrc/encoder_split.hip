@@ -26,8 +26,13 @@
 //   3. accumulates z for its 64 columns (two 32 x 32 blocks).
 // The weights are split and laid out once per weight version by mrp_edge_encoder_pack, in the exact
 // per-lane fragment order, so every weight load of a wave is one contiguous KiB.
-// Work per launch at the headline (E = 1792, C = 512): 224 workgroups of four waves; h is computed
-// once per (32 edges, 64 columns) wave: 6 MFMAs per hidden block against 24 for z.
+// Hidden split (KS = 2, C % 64 == 0): the workgroup's eight waves are two sets of four, each set
+// walking half of the hidden blocks with its own LDS stage ring; the second set's z partials are
+// added to the first's through LDS at the end (a fixed order: deterministic).  Two waves per SIMD
+// then overlap one wave's ReLU/split (VALU) and LDS reads with the other's MFMAs, where one wave per
+// SIMD serialised them, and each wave's dependent chain is half as long.
+// Work per launch at the headline (E = 1792, C = 512): 224 workgroups of 4 KS waves; h is computed
+// once per (32 edges, 64 columns, hidden block): 6 MFMAs per hidden block against 24 for z.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -175,12 +180,12 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   }
 }
 
-template <int CB>
+template <int CB, int KS>
 __device__ __forceinline__ void encoder_body(const FwdArgs& a) {
   using S = Stage<CB>;
   constexpr int NF = S::NP;  // fragments per stage
   constexpr int W1F = 6 * CB;  // first W1 fragment
-  extern __shared__ u4 lds[];
+  extern __shared__ u4 lds_all[];
   // workgroup -> (edge group of 128, column slab of 32 CB); consecutive ids share a slab (its W2
   // image) and, after the remap, an XCD and its L2
   const int nwg = gridDim.x;
@@ -189,14 +194,18 @@ __device__ __forceinline__ void encoder_body(const FwdArgs& a) {
   const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
   const int eg = id % a.egroups, cs = id / a.egroups;
   const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wall = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wv = wall & 3;   // edge block of the workgroup (and DMA slot within the wave set)
+  const int kh = wall >> 2;  // hidden half (KS = 2)
   const int e0 = (eg * 4 + wv) * 32;
-  const int HB = a.C / 32;
+  const int HB = a.C / 32 / KS;   // hidden blocks this wave walks
+  const int hb0 = kh * HB;        // its first
+  u4* lds = lds_all + kh * kStages * S::U4;  // its wave set's stage ring
   const int r = lane & 31, hh = lane >> 5;
 
   // ---- LDS-DMA: wave wv issues pieces wv, wv + 4, ... of every stage (npw of them)
   const int npw = (S::NP - wv + 3) / 4;
-  const int64_t cstride = (int64_t)HB * 2 * 3 * 64;  // 16-B units per W2 column block
+  const int64_t cstride = (int64_t)(a.C / 32) * 2 * 3 * 64;  // 16-B units per W2 column block (all hidden blocks)
   const __amdgpu_buffer_rsrc_t rw = rsrc(a.packed);
   uint32_t voff[S::PW], sstep[S::PW];
 #pragma unroll
@@ -218,7 +227,7 @@ __device__ __forceinline__ void encoder_body(const FwdArgs& a) {
 #pragma unroll
     for (int i = 0; i < S::PW; ++i)
       if (i < npw)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, st + (wv + 4 * i) * 64, 16, voff[i], (uint32_t)hb * sstep[i], 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, st + (wv + 4 * i) * 64, 16, voff[i], (uint32_t)(hb0 + hb) * sstep[i], 0, 0);
   };
   // pose fragment (B operand of X = W1' pose'^T): lane's edge, k = 8 hh + j; k = 9 is the 1.0 of b1
   bf8 pp[3];
@@ -323,6 +332,24 @@ __device__ __forceinline__ void encoder_body(const FwdArgs& a) {
   }
   z_block(F);
 
+  if constexpr (KS == 2) {
+    // the second wave set's partials through LDS (the stage rings are idle: every DMA was waited
+    // for and every fragment read retired before this barrier), added in a fixed order
+    float* zx = reinterpret_cast<float*>(lds_all);
+    __syncthreads();
+    if (kh == 1) {
+#pragma unroll
+      for (int c = 0; c < CB; ++c)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) zx[((wv * CB + c) * 16 + i) * 64 + lane] = Z[c][i];
+    }
+    __syncthreads();
+    if (kh == 1) return;
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) Z[c][i] += zx[((wv * CB + c) * 16 + i) * 64 + lane];
+  }
   // epilogue: accumulator register i of lane (r, hh) is edge e0 + (i & 3) + 8 (i >> 2) + 4 hh, column r
   if (e0 >= a.E) return;  // a wave past the last edge (only the stores are skipped: it took part in the barriers)
   const int N = 2 * a.C;
@@ -338,16 +365,27 @@ __device__ __forceinline__ void encoder_body(const FwdArgs& a) {
   }
 }
 
-// one kernel per column-block count (plain kernels around the template body)
-__global__ void __launch_bounds__(256) encoder_fwd_cb1(FwdArgs a) { encoder_body<1>(a); }
-__global__ void __launch_bounds__(256) encoder_fwd_cb2(FwdArgs a) { encoder_body<2>(a); }
+// one kernel per (column-block count, hidden split) (plain kernels around the template body)
+__global__ void __launch_bounds__(256) encoder_fwd_cb1(FwdArgs a) { encoder_body<1, 1>(a); }
+__global__ void __launch_bounds__(256) encoder_fwd_cb2(FwdArgs a) { encoder_body<2, 1>(a); }
+__global__ void __launch_bounds__(512) encoder_fwd_cb1_k2(FwdArgs a) { encoder_body<1, 2>(a); }
+__global__ void __launch_bounds__(512) encoder_fwd_cb2_k2(FwdArgs a) { encoder_body<2, 2>(a); }
 
-hipError_t launch_fwd(int cb, const FwdArgs& a, int64_t grid, hipStream_t st) {
-  if (cb == 2)
-    hipLaunchKernelGGL(encoder_fwd_cb2, dim3((unsigned)grid), dim3(256), (size_t)kStages * Stage<2>::U4 * 16, st, a);
-  else
-    hipLaunchKernelGGL(encoder_fwd_cb1, dim3((unsigned)grid), dim3(256), (size_t)kStages * Stage<1>::U4 * 16, st, a);
+template <int CB, int KS>
+hipError_t launch_cfg(void (*kern)(FwdArgs), const FwdArgs& a, int64_t grid, hipStream_t st) {
+  const size_t lds = (size_t)KS * kStages * Stage<CB>::U4 * 16;  // >= the KS = 2 exchange (4 CB KiB x 4)
+  static_assert(KS == 1 || (size_t)KS * kStages * Stage<CB>::U4 * 16 >= (size_t)4 * CB * 16 * 64 * 4, "exchange fits");
+  static const hipError_t attr =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256 * KS), lds, st, a);
   return hipGetLastError();
+}
+
+hipError_t launch_fwd(int cb, int ks, const FwdArgs& a, int64_t grid, hipStream_t st) {
+  if (ks == 2)
+    return cb == 2 ? launch_cfg<2, 2>(encoder_fwd_cb2_k2, a, grid, st) : launch_cfg<1, 2>(encoder_fwd_cb1_k2, a, grid, st);
+  return cb == 2 ? launch_cfg<2, 1>(encoder_fwd_cb2, a, grid, st) : launch_cfg<1, 1>(encoder_fwd_cb1, a, grid, st);
 }
 
 }  // namespace mrp_x6
@@ -386,9 +424,17 @@ extern "C" int mrp_edge_encoder_fwd_split(const float* pose, const void* packed,
   a.C = C;
   a.egroups = (num_edges + 127) / 128;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // column blocks per wave: 1 (two workgroups per CU, X recomputed per 32 columns) or 2 (one per CU)
-  const int cb = mrp_host::tuning().edge_split_cb == 2 ? 2 : 1;
+  // column blocks per wave: 1 (two workgroups per CU, X recomputed per 32 columns) or 2 (one per CU);
+  // hidden blocks walked by one wave set or split over two.  Per shape (tools/exp_encoder.py, us,
+  // cb2 k1 / cb2 k2 / cb1 k2): E=1792 C=512 17.4 / 17.7 / 19.7, E=3584 C=512 27.9 / 33.6 / 34.7,
+  // E=768 C=1280 35.6 / 34.3 / 40.6, E=448 C=2048 55.6 / 53.0 / 63.8, E=512 C=1024 28.0 / 26.2 / 20.4:
+  // two column blocks unless that leaves fewer than 192 workgroups, the split from C = 1024 on (the
+  // long hidden walks)
+  const mrp_host::Tuning& tu = mrp_host::tuning();
+  const int cb = tu.edge_split_cb ? tu.edge_split_cb : ((int64_t)a.egroups * (2 * C / 64) >= 192 ? 2 : 1);
+  int ks = tu.edge_split_k ? tu.edge_split_k : (C >= 1024 ? 2 : 1);
+  if ((C / 32) % 2 != 0) ks = 1;  // the split needs an even hidden block count
   const int64_t grid = (int64_t)a.egroups * (2 * (int64_t)C / (32 * cb));
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  return launch_fwd(cb, a, grid, st);
+  return launch_fwd(cb, ks, a, grid, st);
 }

@@ -107,7 +107,8 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"gemm_nt", &t.gemm_nt, -1, 5},
       {"edge_gemm", &t.edge_gemm, 0, 1},
       {"edge_fused", &t.edge_fused, 0, 4},
-      {"edge_split_cb", &t.edge_split_cb, 1, 2},
+      {"edge_split_cb", &t.edge_split_cb, 0, 2},
+      {"edge_split_k", &t.edge_split_k, 0, 2},
       {"gemm_split", &t.gemm_split, -1, 4},
   };
   for (const Knob& k : knobs) {

@@ -34,7 +34,8 @@ struct Tuning {
   int gemm_nn = -1, gemm_nt = -1;  // -1: the per-shape default
   int edge_fused = 2;  // mrp_edge_encoder_fwd variant (compress_gemm.hip MRP_ENC_VARIANTS)
   int gemm_split = -1;  // split-bf16 compress GEMM: -1 per shape, 2 (128-row workgroups) or 4 (256-row)
-  int edge_split_cb = 2;  // mrp_edge_encoder_fwd_split: 32-column blocks per wave (1 or 2)
+  int edge_split_cb = 0;  // mrp_edge_encoder_fwd_split: 32-column blocks per wave (1 or 2; 0 per shape)
+  int edge_split_k = 0;   // mrp_edge_encoder_fwd_split: hidden blocks over 1 or 2 wave sets (0 per shape)
   int edge_gemm = 1;  // edge encoder's second Linear: 64 x 64 tiles of 32 x 32 waves on 16x16x4 (0) or 32x32x2 (1) MFMAs
 };
 Tuning& tuning();

@@ -59,12 +59,13 @@ for name, E, C in SHAPES:
             t = time_launches([lambda: enc.encoder_forward_fused(*args_f)], args.iters, dev)
             row.append(f"fused{v} {t * 1e6:6.1f} us{'' if same else ' MISMATCH'}")
         lib.mrp_tuning_set(b"reset", 0)
-        for cb in (1, 2):
+        for cb, ks in ((1, 1), (2, 1), (1, 2), (2, 2)):
             lib.mrp_tuning_set(b"edge_split_cb", cb)
+            lib.mrp_tuning_set(b"edge_split_k", ks)
             zs = enc.encoder_forward_split(pose, l1, layers[2])
             err = float((zs - ref_full).abs().max() / ref_full.abs().max())
             t = time_launches([lambda: enc.encoder_forward_split(pose, l1, layers[2])], args.iters, dev)
-            row.append(f"split cb{cb} {t * 1e6:6.1f} us (vs fused {err:.1e})")
+            row.append(f"split cb{cb} k{ks} {t * 1e6:6.1f} us (vs fused {err:.1e})")
         lib.mrp_tuning_set(b"reset", 0)
         for path in ("library", "hip", "fused", "split"):
             enc.set_logits_path(path)
