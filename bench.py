@@ -197,23 +197,27 @@ def cpu_baseline(B, N, C, H, W, seconds):
     bucket -> mean) over the headline workload itself, bounded to about ``seconds`` of CPU work."""
     import oracle
     threads, counts = cpu_threads()
+    prev = torch.get_num_threads()
     torch.set_num_threads(threads)
-    g = make_workload(B, N, C, H, W, seed=1234, device="cpu")
-    torch.manual_seed(0)
-    enc = mrp.edge_encoder([C, C])
-    params = dict(enc.named_parameters())
-    src, dst = (t.numpy() for t in g.edges())
-    x = g.ndata["image"]
-    pose = g.edata["pose"]
-    elems = x.numel()
-    with torch.no_grad():
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            oracle.gcn_forward(params, x, pose, src, dst)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el >= seconds:
-                break
+    try:
+        g = make_workload(B, N, C, H, W, seed=1234, device="cpu")
+        torch.manual_seed(0)
+        enc = mrp.edge_encoder([C, C])
+        params = dict(enc.named_parameters())
+        src, dst = (t.numpy() for t in g.edges())
+        x = g.ndata["image"]
+        pose = g.edata["pose"]
+        elems = x.numel()
+        with torch.no_grad():
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                oracle.gcn_forward(params, x, pose, src, dst)
+                reps += 1
+                el = time.perf_counter() - t0
+                if el >= seconds:
+                    break
+    finally:
+        torch.set_num_threads(prev)
     return {"value": elems * reps / el, "unit": "elems/s", "cores": threads, "kind": "port",
             "cpu": cpu_model(), "host": counts,
             "threads_note": "the job's CPU share (OMP_NUM_THREADS, set by the GPU pool to the per-GPU share "
@@ -468,7 +472,35 @@ def config_record(cid, world, rank, device, args):
     return rec
 
 
-def main():
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(argv, gpus: int, port: int):
+    """(argv, env) that start ``gpus`` ranks of this script, one process per GPU, with
+    ``torch.distributed.run`` on 127.0.0.1 — the launch ``bench.py --gpus N`` performs by itself
+    when it is not already running under a launcher (no WORLD_SIZE in the environment)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC: RCCL / tensor sharing across ranks
+    env.pop("WORLD_SIZE", None)
+    return cmd, env
+
+
+def self_launch(argv) -> int:
+    """``--gpus N > 1`` outside a launcher: start the N ranks as child processes and return their
+    exit status (rank 0 prints the JSON line).  Runs before this process touches the GPU."""
+    import subprocess
+    gpus = int(parse_args(argv).gpus)
+    cmd, env = launcher_command(argv, gpus, _free_port())
+    return subprocess.call(cmd, env=env)
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -487,9 +519,17 @@ def main():
     ap.add_argument("--configs", default="0,1,2,3,4", help="BASELINE configs to measure ('' for none)")
     ap.add_argument("--config-steps", type=int, default=10)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (control-flow tests)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(sys.argv[1:]))
 
     rank, world, local = env_rank_world()
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
     ndev = max(torch.cuda.device_count(), 1)
     device = torch.device("cuda", local % ndev)
     torch.cuda.set_device(device)

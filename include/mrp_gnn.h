@@ -323,8 +323,10 @@ int mrp_edge_encoder_fwd(const float* pose, const float* w1, const float* b1, co
  *   mrp_edge_encoder_pack           w1 (C, 9), b1 (C), w2 (2C, C) -> packed (16-byte aligned device buffer)
  *   mrp_edge_encoder_fwd_split      z = relu(pose W1^T + b1) W2^T + b2 from pose (E, 9), the packed image
  *                                   and b2 (2C, or NULL) -> z (E, 2C)
- * Requirements (else hipErrorNotSupported): C % 32 == 0.  Used for inference; training keeps h for its
- * backward and runs mrp_edge_hidden_fwd + mrp_edge_logits_fwd.
+ * Requirements (else hipErrorNotSupported): C % 32 == 0 and a packed image below 2^31 bytes (the
+ * kernel addresses it with 32-bit offsets: C <= 13344).  The z accumulation keeps the a0 b0 products
+ * apart from the five small ones (two accumulators per output, summed once).  Used for inference;
+ * training keeps h for its backward and runs mrp_edge_hidden_fwd + mrp_edge_logits_fwd.
  */
 int64_t mrp_edge_encoder_pack_bytes(int32_t C);
 int mrp_edge_encoder_pack(const float* w1, const float* b1, const float* w2, int32_t C, void* packed, void* stream);
@@ -378,8 +380,9 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * variant table); "edge_gemm" (1, default: mrp_edge_logits_fwd on 32x32x2 MFMAs; 0: 16x16x4); "edge_fused"
  * (mrp_edge_encoder_fwd tile/buffer variant, 0..4); "edge_split_cb" (mrp_edge_encoder_fwd_split: 32-column
  * blocks per wave, 1 or 2; 0, default: per shape); "edge_split_k" (its hidden blocks over 1 or 2
- * wave sets, 2 only when C % 64 == 0; 0, default: per shape); "gemm_split" (split-bf16 compress GEMM workgroup: -1 per shape,
- * 2 = 128 rows / 4 waves, 4 = 256 rows / 8 waves). */
+ * wave sets, 2 only when C % 64 == 0; 0, default: per shape); "gemm_split" (split-bf16 compress
+ * forward / data-gradient kernel: -1 per shape, 2 = 128 rows / 4 waves, 4 = 256 rows / 8 waves with
+ * 32-k stages, 5 = 256 rows / 8 waves, pipelined 16-k stages; any other value is rejected). */
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 16 = this header: v15 plus

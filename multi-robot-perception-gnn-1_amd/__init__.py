@@ -13,7 +13,8 @@ from . import compat, compress, encoder  # noqa: F401
 from .device_graph import frame_batch  # noqa: F401
 from .graph import (GraphCSR, RobotGraph, batch, complete_edges, complete_graph, frame_graph,  # noqa: F401
                     graph, knn_edges, load_graphs, save_graphs, unbatch)
-from .models import GCN, GCNBlock, GCNStack, edge_encoder, multi_view_dgl_model, stack_layout  # noqa: F401
+from .models import (GCN, GCNBlock, GCNStack, clear_packed_weights, edge_encoder, multi_view_dgl_model,  # noqa: F401
+                     stack_layout)
 from .pose import cal_relative_pose, quat_to_so3, relative_pose_batch  # noqa: F401
 
 __version__ = "0.1.0"

@@ -192,17 +192,27 @@ def compress_backward_data(weight: torch.Tensor, gy: torch.Tensor, gx: torch.Ten
     return gx, ga
 
 
-def compress_backward_weight(gy: torch.Tensor, x: torch.Tensor, a: torch.Tensor, want_bias: bool = True):
+def compress_backward_weight(gy: torch.Tensor, x: torch.Tensor, a: torch.Tensor, want_bias: bool = True,
+                             weight: torch.Tensor = None, bias: torch.Tensor = None):
     """(dW (C, 2C, 1, 1), db (C) or None) = (sum_n gy[n] [x[n]; a[n]]^T, sum gy)
-    (``mrp_compress_bwd_weight``); None when the kernel declines the shape (H W % 32 != 0)."""
+    (``mrp_compress_bwd_weight``); None when the kernel declines the shape (H W % 32 != 0).  Given
+    the parameters, the results are written straight into a gradient all-reducer's buckets when
+    one holds them (``dist.grad_out_like``)."""
     from .aggregate import _ptr, _stream
+    from .dist import grad_out_like
     n, C, H, W = gy.shape
     lib = _lib.load_library()
     gy, gs = _node_major(gy)
     x, xs = _node_major(x)
     a, as_ = _node_major(a)
-    dw = torch.empty((C, 2 * C, 1, 1), device=gy.device, dtype=torch.float32)
-    db = torch.empty((C,), device=gy.device, dtype=torch.float32) if want_bias else None
+    dw = grad_out_like(weight) if weight is not None and weight.dim() == 4 else None
+    if dw is None:
+        dw = torch.empty((C, 2 * C, 1, 1), device=gy.device, dtype=torch.float32)
+    db = None
+    if want_bias:
+        db = grad_out_like(bias) if bias is not None else None
+        if db is None:
+            db = torch.empty((C,), device=gy.device, dtype=torch.float32)
     P = H * W
     split = _split("wgrad") and C % 64 == 0 and P % 32 == 0
     if split:
@@ -336,14 +346,14 @@ class FilmCompressFunction(torch.autograd.Function):
         film_mean_forward_into(x, gb, csr, mode, agg)
         hip = _use_kernels(C, H * W)
         y = compress_forward(weight, bias, x, agg) if hip else _lib_forward(weight, bias, x, agg)
-        ctx.save_for_backward(x, gb, agg, weight)
+        ctx.save_for_backward(x, gb, agg, weight, bias)
         ctx.csr, ctx.mode, ctx.has_bias, ctx.hip = csr, mode, bias is not None, hip
         return y
 
     @staticmethod
     def backward(ctx, gy):
         from .aggregate import film_mean_backward
-        x, gb, agg, weight = ctx.saved_tensors
+        x, gb, agg, weight, bias = ctx.saved_tensors
         need_x, need_gb = ctx.needs_input_grad[0], gb is not None and ctx.needs_input_grad[1]
         dx = dgb = dw = db = None
         if need_x or need_gb:
@@ -353,7 +363,7 @@ class FilmCompressFunction(torch.autograd.Function):
             if dgb is not None:
                 dgb = dgb.view(gb.shape).to(gb.dtype)
         if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
-            r = compress_backward_weight(gy, x, agg, ctx.has_bias) if ctx.hip else None
+            r = compress_backward_weight(gy, x, agg, ctx.has_bias, weight, bias) if ctx.hip else None
             dw, db = r if r is not None else _lib_backward_weight(gy, x, agg, ctx.has_bias)
             if not ctx.needs_input_grad[2]:
                 dw = None

@@ -307,6 +307,311 @@ __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
 __global__ void __launch_bounds__(256, 1) gemm_nn_split_w2(Args a) { gemm_nn_split_body<2>(a); }
 __global__ void __launch_bounds__(512, 1) gemm_nn_split_w4(Args a) { gemm_nn_split_body<4>(a); }
 
+// ------------------------------------------------------------------------------------------------
+// Pipelined NN form (256 x 128 tiles, 8 waves of 64 x 64): stages of ONE 16-k step in a ring of
+// NBUF = L + 2 LDS buffers; stage t's operands are requested L stages before they are needed.
+// Per stage s a wave
+//   - waits for its own requests of stage s + 2 (issued at stage s - L: counted vmcnt, the younger
+//     requests stay in flight), splits its B piece of stage s + 2 into buffer (s + 2) % NBUF, then
+//     requests stage s + 2 + L: its A pieces by LDS-DMA into buffer (s + 2 + L) % NBUF and its B
+//     piece into the registers the split just freed (L register sets);
+//   - runs stage s's 24 MFMAs (fragments already in registers) and, as each fragment's last MFMA
+//     issues, reads the same fragment of stage s + 1 into its registers (no second fragment set);
+//   - waits for its LDS writes, barrier: stage s + 2 is complete for every wave.
+// Buffer (s + 2 + L) % NBUF = s % NBUF held stage s, whose fragments were read during stage s - 1
+// (before the barrier that ended it); buffer (s + 2) % NBUF held stage s + 2 - NBUF = s - L, read
+// during stage s - L - 1.  One barrier per 24 MFMAs; after it the MFMAs start at once.
+// The B pieces travel by LDS-DMA too (global_load_lds, one 16-byte piece per lane into a raw fp32
+// slot; each thread reads back exactly the piece its own lane requested, so its own counted vmcnt
+// orders the read): hipcc waits vmcnt(0) before the first use of an ordinary load's result whenever
+// an LDS-DMA is in flight (cdna_hip_programming.md, "Pipelining across barriers"), which would drain
+// the pipeline every stage.  Every wait is explicit and counted (per stage, in issue order: the 3 A
+// pieces, then the B piece).
+// ------------------------------------------------------------------------------------------------
+template <int WMW, int L>
+struct Geo3 {
+  static constexpr int TM = 64 * WMW, NW = 2 * WMW, THREADS = 64 * NW;
+  static constexpr int BKS = 16;                     // k per stage
+  static constexpr int A_PIECES = (TM / 32) * 3;     // 1 KiB pieces per stage
+  static constexpr int A_BYTES = A_PIECES * 1024;
+  static constexpr int B_PART = BKS * TN * 2;        // one bf16 part of the B stage: 4 KiB
+  static constexpr int BUF_BYTES = A_BYTES + 3 * B_PART;
+  static constexpr int NBUF = L + 2;
+  static constexpr int B_RAW = BKS * TN * 4;         // the fp32 B stage as loaded: 8 KiB
+  static constexpr int RAW_OFF = NBUF * BUF_BYTES;   // L raw B slots after the ring
+  static constexpr int LDS_BYTES = RAW_OFF + L * B_RAW;  // 160 KiB at WMW 4, L 2
+  static constexpr int PPW = A_PIECES / NW;          // DMA pieces per wave per stage
+  static constexpr int BJ = BKS * TN / 4 / THREADS;  // 16-byte B pieces per thread per stage
+  static constexpr int KR = THREADS / 32;            // B rows per pass
+  static constexpr int OPS = PPW + BJ;               // vector-memory requests per wave per stage
+  static_assert(BJ * THREADS * 4 == BKS * TN, "whole B pieces per thread");
+  static_assert(A_PIECES % NW == 0, "whole DMA pieces per wave");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+};
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+template <int WMW, int L, int ABL = 0>  // ABL: lab ablation bits (tools/gemm_ablate.hip; 0 in the library)
+__device__ __forceinline__ void gemm_nn_split3_body(const Args& a) {
+  using G = Geo3<WMW, L>;
+  constexpr int TM = G::TM, NW = G::NW, A_BYTES = G::A_BYTES, BUF_BYTES = G::BUF_BYTES, B_PART = G::B_PART;
+  constexpr int NBUF = G::NBUF, OPS = G::OPS;
+  static_assert(L == 1 || L == 2, "one or two stages of request lead");
+  extern __shared__ u4 lds[];
+  char* ldsb = reinterpret_cast<char*>(lds);
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int mt = id % a.mtiles, nt = id / a.mtiles;
+  const int64_t nbase = (int64_t)nt * TN;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int nst = a.K / 16, ks0 = a.k0 / 16, MB = a.M / 32;
+
+  // ---- A: LDS-DMA pieces pc = mbl 3 + p (local m block, part), pc = w + NW i
+  const __amdgpu_buffer_rsrc_t ra = rsrc(a.ap);
+  uint32_t va[G::PPW];
+#pragma unroll
+  for (int i = 0; i < G::PPW; ++i) {
+    const int pc = w + NW * i;
+    const int mbl = pc / 3, p = pc % 3;
+    const int mb = min(mt * (TM / 32) + mbl, MB - 1);  // blocks past M: any valid data, never stored
+    va[i] = (uint32_t)((((int64_t)mb * nst * 3 + p) * 64 + lane) * 16);
+  }
+  auto issue_a = [&](int s, int buf) {
+#pragma unroll
+    for (int i = 0; i < G::PPW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, lds + (buf * BUF_BYTES + (w + NW * i) * 1024) / 16, 16, va[i],
+                                               (uint32_t)s * 3 * 1024, 0, 0);
+  };
+
+  // ---- B: thread t loads the 16-byte pieces (rows (t >> 5) + KR j, columns 4 (t & 31) ..) of a stage
+  constexpr int BJ = G::BJ, KR = G::KR;
+  const int fc = threadIdx.x & 31, kr = threadIdx.x >> 5;
+  int64_t col = nbase + 4 * fc;
+  if (col > a.ncols - 4) col = a.ncols - 4;  // columns past the end: any valid data, never stored
+  const int64_t node = col / a.P, pix = col - node * a.P;
+  // buffer resources based at the tile's first node and the stage's first channel (scalar, rebuilt
+  // per stage), so a lane's offset spans at most the tile's few nodes (global_load_lds would be a
+  // FLAT-encoded load, after which hipcc waits lgkmcnt(0) before the next MFMA)
+  const int64_t node0 = nbase / a.P;
+  uint32_t vb0[BJ], vb1[BJ];
+#pragma unroll
+  for (int j = 0; j < BJ; ++j) {
+    vb0[j] = (uint32_t)(((node - node0) * a.b0s + pix + (int64_t)(kr + KR * j) * a.P) * 4);
+    vb1[j] = (uint32_t)(((node - node0) * a.b1s + pix + (int64_t)(kr + KR * j) * a.P) * 4);
+  }
+  const float* const bb0 = a.b0 + node0 * a.b0s;
+  const float* const bb1 = a.b1 + node0 * a.b1s;
+  char* const raw = ldsb + G::RAW_OFF;
+  // piece j of thread t lands at raw + slot B_RAW + 16 (j THREADS + t)
+  auto load_b = [&](int s, int slot) {
+    const bool lo = s < ks0;
+    const __amdgpu_buffer_rsrc_t rb = rsrc(lo ? bb0 + (int64_t)s * 16 * a.P : bb1 + (int64_t)(s - ks0) * 16 * a.P);
+#pragma unroll
+    for (int j = 0; j < BJ; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, lds + (G::RAW_OFF + slot * G::B_RAW + j * G::THREADS * 16 + w * 1024) / 16, 16, lo ? vb0[j] : vb1[j], 0,
+          0, 0);
+  };
+  // the raw read by inline asm too (a compiler-visible read there makes hipcc wait for it before the
+  // first MFMA of the stage); its result is guarded by an asm lgkmcnt wait naming the registers,
+  // which must precede every use
+  const uint32_t raw_addr = (uint32_t)reinterpret_cast<uintptr_t>(raw + 16 * threadIdx.x);
+  struct Raw {
+    f4 v[BJ];
+  };
+  auto raw_b = [&](int slot) {
+    Raw r;
+#pragma unroll
+    for (int j = 0; j < BJ; ++j)
+      asm volatile("ds_read_b128 %0, %1 offset:%2"
+                   : "=v"(r.v[j])
+                   : "v"(raw_addr + (uint32_t)(slot * G::B_RAW)), "i"(j * G::THREADS * 16)
+                   : "memory");
+    return r;
+  };
+  auto raw_wait = [&](Raw& r) {
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r.v[j])::"memory");
+  };
+  auto store_b = [&](const Raw& r, int buf) {
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) {
+      char* bimg = ldsb + buf * BUF_BYTES + A_BYTES + boff(kr + KR * j, fc >> 1) + 8 * (fc & 1);
+      u2 p0, p1, p2;
+      f2 lo, hi;
+      lo.x = r.v[j].x, lo.y = r.v[j].y, hi.x = r.v[j].z, hi.y = r.v[j].w;
+      uint32_t l0, l1, l2, h0, h1, h2;
+      split2(lo, l0, l1, l2);
+      split2(hi, h0, h1, h2);
+      p0.x = l0, p1.x = l1, p2.x = l2, p0.y = h0, p1.y = h1, p2.y = h2;
+      *reinterpret_cast<u2*>(bimg) = p0;
+      *reinterpret_cast<u2*>(bimg + B_PART) = p1;
+      *reinterpret_cast<u2*>(bimg + 2 * B_PART) = p2;
+    }
+  };
+
+  // ---- fragment reads: A by row pieces (ds_read_b128), B by ds_read_b64_tr_b16
+  const int g16 = lane >> 4, i16 = lane & 15, hh = lane >> 5;
+  const int trq = i16 >> 2, trp = i16 & 3;
+  bf8 af[2][3], bfr[2][3];
+  auto read_a = [&](int buf, int mi) {
+    const char* base = ldsb + buf * BUF_BYTES + lane * 16;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      af[mi][p] = __builtin_bit_cast(bf8, *reinterpret_cast<const u4*>(base + ((2 * wm + mi) * 3 + p) * 1024));
+  };
+  // B fragments by inline-asm ds_read_b64_tr_b16: the builtin carries no memory operand, so hipcc
+  // would wait for every LDS-DMA in flight (vmcnt(0)) before it, though the DMA fills another buffer;
+  // the waits these reads need are placed by hand below (LDS operations retire in order)
+  uint32_t tra[2][2];  // byte address of read (ni, t) in buffer 0, part 0
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int row = 8 * hh + 4 * t + trq;
+      const int ch = (64 * wn + 32 * ni + 16 * (g16 & 1)) / 8 + (trp >> 1);
+      tra[ni][t] = (uint32_t)reinterpret_cast<uintptr_t>(ldsb + A_BYTES + boff(row, ch) + 8 * (trp & 1));
+    }
+  auto read_b = [&](int buf, int ni) {
+    const uint32_t o = (uint32_t)(buf * BUF_BYTES);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      s4 v[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v[t]) : "v"(tra[ni][t] + o), "i"(p * B_PART));
+      u4 u;
+      u.x = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[0], v[0], 0, 1));
+      u.y = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[0], v[0], 2, 3));
+      u.z = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[1], v[1], 0, 1));
+      u.w = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[1], v[1], 2, 3));
+      bfr[ni][p] = __builtin_bit_cast(bf8, u);
+    }
+  };
+
+  Acc2 acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni].hi[r] = acc[mi][ni].lo[r] = 0.f;
+
+  // ---- prologue: stages 0 and 1 complete in buffers 0 and 1; stages 2 .. 1 + L requested (stage
+  // t's raw B piece in slot t % L)
+  issue_a(0, 0);
+  load_b(0, 0);
+  vm_wait<0>();
+  Raw v0 = raw_b(0);
+  raw_wait(v0);
+  store_b(v0, 0);
+  issue_a(1, 1);  // nst >= 2 (K % 32 == 0)
+  load_b(1, L - 1);
+  vm_wait<0>();
+  Raw v1 = raw_b(L - 1);
+  raw_wait(v1);
+  store_b(v1, 1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the raw reads retired before the slots refill
+#pragma unroll
+  for (int t = 2; t < 2 + L; ++t)
+    if (t < nst) {
+      issue_a(t, t);
+      load_b(t, t % L);
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  read_a(0, 0);
+  read_a(0, 1);
+  read_b(0, 0);
+  read_b(0, 1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  // Fragment reads of stage s + 1 (LDS operations in issue order): group 2 = A block 0 (3 reads),
+  // group 3 = B block 0 (6), group 4 = A block 1 + B block 1 (9).  The barrier that ends stage s waits
+  // for all but group 4; the MFMAs of block (0, 1) of stage s + 1 wait for group 4 too.
+  auto stage = [&](int s, int slot) {  // slot = (s + 2) % L: stage s + 2's raw B piece, then s + 2 + L's
+    const int cur = s % NBUF;
+    const int nxt = cur + 1 == NBUF ? 0 : cur + 1;   // stage s + 1 (past the last stage: never used)
+    const int fil = nxt + 1 == NBUF ? 0 : nxt + 1;   // stage s + 2
+    // stage s + 2's requests (issued L stages ago) landed; each later stage issued OPS requests.
+    // Past the last stage the raw read and the split are harmless: the split goes to a buffer no
+    // wave reads again (stage s + 2 - NBUF's, read during stage s + 1 - NBUF)
+    if (L == 2 && s + 3 < nst)
+      vm_wait<OPS>();
+    else
+      vm_wait<0>();
+    Raw v = raw_b(slot);  // its latency runs under the first six MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    mma6(af[0], bfr[0], acc[0][0]);
+    __builtin_amdgcn_sched_barrier(0);
+    raw_wait(v);  // the raw read (and all older LDS reads)
+    if (!(ABL & 8)) store_b(v, fil);
+    if (s + 2 + L < nst) {
+      if (!(ABL & 1)) issue_a(s + 2 + L, cur);  // buffer s % NBUF: stage s's fragments are in registers
+      if (!(ABL & 2)) load_b(s + 2 + L, slot);  // after the split consumed the slot's piece
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // group 4 of the previous stage retired (stage s's B block 1; the raw read above retired with
+    // it); the LDS writes may not have (2 or 3 instructions per piece: hipcc may pair two of them)
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * BJ) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma6(af[0], bfr[1], acc[0][1]);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(nxt, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma6(af[1], bfr[0], acc[1][0]);
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(nxt, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma6(af[1], bfr[1], acc[1][1]);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(nxt, 1);
+    read_b(nxt, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    // every LDS operation but group 4 retired: stage s + 2 is complete for all waves after the
+    // barrier, and no wave writes a buffer another may still read
+    asm volatile("s_waitcnt lgkmcnt(9)" ::: "memory");
+    if (!(ABL & 4)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#pragma unroll 1
+  for (int s = 0; s < nst; ++s) stage(s, L == 2 ? s & 1 : 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the (unused) reads past the last stage
+
+  // ---- epilogue (as gemm_nn_split_body)
+  const int mbase = mt * TM + 64 * wm;
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int64_t n = nbase + 64 * wn + 32 * ni + (lane & 31);
+    if (n >= a.ncols) continue;
+    const int64_t nd = n / a.P, px = n - nd * a.P;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mbase + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (m >= a.M) continue;
+        float v = __fadd_rn(acc[mi][ni].hi[r], acc[mi][ni].lo[r]);
+        if (a.bias != nullptr) v = __fadd_rn(v, a.bias[m]);
+        float* dst = m < a.m0 ? a.c0 + nd * a.c0s + (int64_t)m * a.P + px
+                              : a.c1 + nd * a.c1s + (int64_t)(m - a.m0) * a.P + px;
+        *dst = v;
+      }
+  }
+}
+
+__global__ void __launch_bounds__(512, 1) gemm_nn_split3_w4(Args a) { gemm_nn_split3_body<4, 2>(a); }
+// 128-row workgroups of 4 waves, two per CU (80 KiB of LDS each): the two workgroups' barriers and
+// request bursts are independent, so one's run under the other's MFMAs
+__global__ void __launch_bounds__(256, 2) gemm_nn_split3_w2(Args a) { gemm_nn_split3_body<2, 1>(a); }
+
 constexpr int64_t kOffMax = (int64_t)1 << 31;
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -317,7 +622,23 @@ hipError_t launch_w(Args a, hipStream_t st, const void* fn, void (*kern)(Args)) 
   a.mtiles = (a.M + G::TM - 1) / G::TM;
   const int64_t grid = (int64_t)a.mtiles * ((a.ncols + TN - 1) / TN);
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  hipError_t attr = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+  static const hipError_t attr = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
+  return hipGetLastError();
+}
+
+template <int WMW, int L>
+hipError_t launch3(Args a, hipStream_t st, void (*kern)(Args)) {
+  using G = Geo3<WMW, L>;
+  // the B operands' buffer offsets span a column tile's nodes (+ one for a ragged tile): 32-bit
+  const int64_t span = ((int64_t)TN / a.P + 2) * (a.b0s > a.b1s ? a.b0s : a.b1s) * 4;
+  if (span >= kOffMax) return hipErrorNotSupported;
+  a.mtiles = (a.M + G::TM - 1) / G::TM;
+  const int64_t grid = (int64_t)a.mtiles * ((a.ncols + TN - 1) / TN);
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
   if (attr != hipSuccess) return attr;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
   return hipGetLastError();
@@ -326,9 +647,17 @@ hipError_t launch_w(Args a, hipStream_t st, const void* fn, void (*kern)(Args)) 
 hipError_t launch(Args a, hipStream_t st) {
   if (a.K % BK != 0 || a.k0 % BK != 0 || a.M % 32 != 0 || a.P % 4 != 0) return hipErrorNotSupported;
   if ((int64_t)a.M * a.K * 6 >= kOffMax) return hipErrorNotSupported;
-  // 256-row workgroups (8 waves, two per SIMD: one splits and stages while the other multiplies, and
-  // each B stage serves twice the rows) when M is a multiple of 256, else 128-row ones
-  const int v = mrp_host::tuning().gemm_split;
+  // 256-row workgroups (8 waves, two per SIMD, each B stage split once for 256 rows) when M is a
+  // multiple of 256: the pipelined form (5) by default — bit-identical to the 32-k-stage form (4), 3-11 %
+  // faster at every config shape (tools/gemm_lab.cpp: configs[3] forward 189 -> 210 TF/s) — else
+  // 128-row ones.  6 (two 4-wave workgroups per CU, pipelined) measured no faster than 4 and is a lab
+  // variant.
+  int v = mrp_host::tuning().gemm_split;
+  if (v < 0 && a.M % 256 == 0) v = 5;
+  if (v == 5 || v == 6) {
+    const hipError_t e = v == 5 ? launch3<4, 2>(a, st, gemm_nn_split3_w4) : launch3<2, 1>(a, st, gemm_nn_split3_w2);
+    if (e != hipErrorNotSupported) return e;
+  }
   const bool wide = v == 4 || (v < 0 && a.M % 256 == 0);
   return wide ? launch_w<4>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w4), gemm_nn_split_w4)
               : launch_w<2>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w2), gemm_nn_split_w2);
@@ -698,11 +1027,11 @@ extern "C" int mrp_compress_bwd_weight_split(const float* gy, int64_t gy_node_st
   a.P = P;
   const int64_t grid = (int64_t)a.mtiles * a.ntiles * ns;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split_w4),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
-  if (e != hipSuccess) return e;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split_w4),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+  if (attr != hipSuccess) return attr;
   hipLaunchKernelGGL(gemm_nt_split_w4, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess || ns == 1) return e;
   const int64_t n4 = M * N / 4;
   const int64_t blocks = (n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048;

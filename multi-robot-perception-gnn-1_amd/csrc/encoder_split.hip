@@ -88,7 +88,22 @@ __device__ __forceinline__ float relu(float x) { return __int_as_float(max(__flo
 __device__ __forceinline__ bf8 as_bf8(u4 v) { return __builtin_bit_cast(bf8, v); }
 __device__ __forceinline__ u4 as_u4(bf8 v) { return __builtin_bit_cast(u4, v); }
 
-// acc += a b over the split parts: the six products with i + j <= 2, smallest first
+// The z accumulation (K = C, up to 128 16-k steps at C = 2048) keeps a0 b0 in its own accumulator
+// and the five small products (at most 2^-8 of the product) in a second one, summed once in the
+// epilogue: the long accumulation then sees a sixth of the additions into the large sum, as in the
+// compress GEMMs (compress_split.hip, Acc2), whose pixel sums drifted 6x the fp32 GEMM's error with
+// one accumulator (tests/test_gpu_encoder.py checks the column sums of z at C = 2048).
+__device__ __forceinline__ void mma6_2(const bf8 (&a)[3], const bf8 (&b)[3], f16v& hi, f16v& lo) {
+  lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], lo, 0, 0, 0);
+  hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], hi, 0, 0, 0);
+}
+
+// acc += a b over the split parts: the six products with i + j <= 2, smallest first (one 16-k step:
+// the hidden layer, K = 9 + bias)
 __device__ __forceinline__ f16v mma6(const bf8 (&a)[3], const bf8 (&b)[3], f16v acc) {
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
@@ -250,11 +265,11 @@ __device__ __forceinline__ void encoder_body(const FwdArgs& a) {
   issue(0);
   if (HB > 1) issue(1);
 
-  f16v Z[CB];
+  f16v Z[CB], ZL[CB];  // z: a0 b0 products, the five small ones
 #pragma unroll
   for (int c = 0; c < CB; ++c)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) Z[c][i] = 0.f;
+    for (int i = 0; i < 16; ++i) Z[c][i] = ZL[c][i] = 0.f;
   bf8 hp[2][3];  // the previous block's ReLU'd hidden values, split (A operand per 16-unit step)
 
   // Stage hb landed (own pieces; the younger stage hb + 1 may still be in flight), then the barrier
@@ -298,7 +313,7 @@ __device__ __forceinline__ void encoder_body(const FwdArgs& a) {
         bf8 wb[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) wb[p] = as_bf8(w[6 * c + 3 * s + p]);
-        Z[c] = mma6(hp[s], wb, Z[c]);
+        mma6_2(hp[s], wb, Z[c], ZL[c]);
       }
   };
 
@@ -331,6 +346,10 @@ __device__ __forceinline__ void encoder_body(const FwdArgs& a) {
     for (int k = 0; k < NF; ++k) F[k] = G[k];
   }
   z_block(F);
+#pragma unroll
+  for (int c = 0; c < CB; ++c)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Z[c][i] = __fadd_rn(Z[c][i], ZL[c][i]);
 
   if constexpr (KS == 2) {
     // the second wave set's partials through LDS (the stage rings are idle: every DMA was waited
@@ -392,6 +411,12 @@ hipError_t launch_fwd(int cb, int ks, const FwdArgs& a, int64_t grid, hipStream_
 
 using namespace mrp_x6;
 
+namespace {
+// the kernels address the packed image with 32-bit byte offsets (buffer resource, num_records
+// 0x7fffffff): the image (96 C + 12 C^2 bytes) must stay below 2^31 bytes, i.e. C <= 13344
+bool image_fits(int32_t C) { return (w1_units(C) + w2_units(C)) * 16 < ((int64_t)1 << 31); }
+}  // namespace
+
 extern "C" int64_t mrp_edge_encoder_pack_bytes(int32_t C) {
   if (C <= 0 || C % 32 != 0) return 0;
   return (w1_units(C) + w2_units(C)) * 16;
@@ -400,7 +425,7 @@ extern "C" int64_t mrp_edge_encoder_pack_bytes(int32_t C) {
 extern "C" int mrp_edge_encoder_pack(const float* w1, const float* b1, const float* w2, int32_t C, void* packed,
                                      void* stream) {
   if (C <= 0) return hipErrorInvalidValue;
-  if (C % 32 != 0) return hipErrorNotSupported;
+  if (C % 32 != 0 || !image_fits(C)) return hipErrorNotSupported;
   if (!w1 || !b1 || !w2 || !packed || (reinterpret_cast<uintptr_t>(packed) & 15)) return hipErrorInvalidValue;
   const int64_t threads = (w1_units(C) + w2_units(C)) / 3;
   if ((threads + 255) / 256 > 0x7fffffff) return hipErrorInvalidValue;
@@ -413,7 +438,7 @@ extern "C" int mrp_edge_encoder_fwd_split(const float* pose, const void* packed,
                                           int32_t C, float* z, void* stream) {
   if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
   if (num_edges == 0 || C == 0) return hipSuccess;
-  if (C % 32 != 0) return hipErrorNotSupported;
+  if (C % 32 != 0 || !image_fits(C)) return hipErrorNotSupported;
   if (!pose || !packed || !z || (reinterpret_cast<uintptr_t>(packed) & 15)) return hipErrorInvalidValue;
   FwdArgs a;
   a.pose = pose;

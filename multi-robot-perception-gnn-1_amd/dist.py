@@ -27,6 +27,7 @@ of silently reducing a partial sum.
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Iterable, List, Optional, Tuple
 
 import torch
@@ -81,8 +82,33 @@ def shard_graph(g, rank: int, world: int):
     return sub, (lo, hi)
 
 
+#: live reducers, consulted by the backward kernels' output allocation (:func:`grad_out_like`)
+_ACTIVE = weakref.WeakSet()
+
+
+def grad_out_like(param: torch.Tensor) -> Optional[torch.Tensor]:
+    """Where a backward kernel should write ``param``'s gradient: a fresh view of the slot a live
+    :class:`GradAllReducer` keeps for it in its flat bucket, or None (allocate normally).  Autograd's
+    AccumulateGrad then adopts the returned tensor as ``param.grad`` without a copy (a freshly made,
+    unshared tensor with the parameter's layout), so the gradient is already in the all-reduce
+    buffer.  Handed out once per step and only while ``param.grad`` is None (a gradient that
+    accumulates onto an existing one is written elsewhere and added by autograd as usual)."""
+    for red in list(_ACTIVE):
+        v = red.claim(param)
+        if v is not None:
+            return v
+    return None
+
+
 class GradAllReducer:
-    """Bucketed, backward-overlapped gradient averaging over a process group."""
+    """Bucketed, backward-overlapped gradient averaging over a process group.
+
+    Every bucket is one preallocated flat buffer and every parameter's ``.grad`` is a view into it
+    (the gradient-as-bucket-view layout): the all-reduce runs in place on the gradients themselves,
+    with no per-step concatenation and no copy back.  A gradient that autograd allocated on its
+    own (``zero_grad(set_to_none=True)`` and an op that did not write through :func:`grad_out_like`)
+    is copied into its slot once, in the hook; with ``set_to_none=False`` autograd accumulates
+    straight into the views.  ``copies`` counts those hook copies (tests)."""
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 32 << 20,
                  group: Optional[dist.ProcessGroup] = None):
@@ -100,12 +126,20 @@ class GradAllReducer:
             size += nbytes
         if cur:
             self.buckets.append(cur)
-        self._bucket_of = {}
+        self._slot = {}    # id(p) -> (bucket, offset, numel)
+        self._by_ptr = {}  # parameter storage address -> parameter (grad_out_like lookups)
+        self._flat: List[torch.Tensor] = []
         for bi, b in enumerate(self.buckets):
+            off = 0
             for p in b:
-                self._bucket_of[id(p)] = bi
+                self._slot[id(p)] = (bi, off, p.numel())
+                self._by_ptr[(p.data_ptr(), p.device)] = p
+                off += p.numel()
+            self._flat.append(torch.zeros(off, dtype=b[0].dtype, device=b[0].device))
+        self._bucket_of = {k: v[0] for k, v in self._slot.items()}
         self._scale = 1.0 / self.world
         self._empty = False  # this rank holds no graphs this step (set_local_count(0))
+        self.copies = 0
         #: (event, bucket) in the order they happen during a backward: ("grad", b) when a parameter's
         #: gradient lands, ("launch", b) when a bucket's all-reduce is started; ``last_events`` is the
         #: record of the last synchronized step — the evidence that the all-reduces overlap backward
@@ -114,6 +148,7 @@ class GradAllReducer:
         self.last_events: List[Tuple[str, int]] = []
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
         self.reset()
+        _ACTIVE.add(self)
 
     def set_local_count(self, n_local: int) -> float:
         """This rank holds ``n_local`` of the step's graphs (its loss a mean over them): scale its
@@ -134,11 +169,39 @@ class GradAllReducer:
             return b[0].device
         return torch.device("cpu")
 
+    def view(self, p: torch.Tensor) -> torch.Tensor:
+        """``p``'s slot in its bucket's flat buffer, shaped like ``p`` (a new view object)."""
+        bi, off, n = self._slot[id(p)]
+        return self._flat[bi][off:off + n].view_as(p)
+
+    def claim(self, t: torch.Tensor) -> Optional[torch.Tensor]:
+        """:func:`grad_out_like` for this reducer's parameters (see there)."""
+        p = self._by_ptr.get((t.data_ptr(), t.device))
+        if p is None or p.shape != t.shape or p.grad is not None or id(p) in self._handed \
+                or self._work[self._bucket_of[id(p)]] is not None:
+            return None
+        self._handed.add(id(p))
+        return self.view(p)
+
     def reset(self) -> None:
         self.events = []
         self._pending = [len(b) for b in self.buckets]
         self._work = [None] * len(self.buckets)
-        self._flat = [None] * len(self.buckets)
+        self._landed = set()
+        self._handed = set()
+
+    def _adopt(self, p: torch.Tensor) -> None:
+        """Make ``p.grad`` its bucket slot (copying a gradient that lives elsewhere; zeros if none)."""
+        v = self.view(p)
+        g = p.grad
+        if g is None:
+            v.zero_()
+        elif g.data_ptr() != v.data_ptr():
+            v.copy_(g)
+            self.copies += 1
+        else:
+            return
+        p.grad = v
 
     def _on_grad(self, p: torch.Tensor) -> None:
         bi = self._bucket_of[id(p)]
@@ -147,39 +210,32 @@ class GradAllReducer:
                                "(more than one backward before synchronize()); call synchronize() after "
                                "every backward")
         self.events.append(("grad", bi))
+        self._adopt(p)
+        self._landed.add(id(p))
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._launch(bi)
 
     def _launch(self, bi: int) -> None:
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.buckets[bi]]
-        flat = torch.cat([g.reshape(-1) for g in grads])
+        for p in self.buckets[bi]:
+            if id(p) not in self._landed:  # no gradient this step (an unused parameter)
+                self._adopt(p)
+        flat = self._flat[bi]
         if self._empty:
             flat.zero_()
         else:
             flat.mul_(self._scale)  # n_r / N (or 1 / P): the SUM all-reduce then yields the average
         self.events.append(("launch", bi))
-        self._flat[bi] = flat
         self._work[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def synchronize(self) -> None:
         """Wait for every bucket (launching any whose hooks did not all fire, e.g. unused
-        parameters) and write the averaged gradients back."""
+        parameters); the averaged gradients are then in every ``p.grad`` (views of the buckets)."""
         for bi in range(len(self.buckets)):
             if self._work[bi] is None:
                 self._launch(bi)
-        for bi, b in enumerate(self.buckets):
+        for bi in range(len(self.buckets)):
             self._work[bi].wait()
-            flat = self._flat[bi]
-            off = 0
-            for p in b:
-                n = p.numel()
-                g = flat[off:off + n].view_as(p)
-                if p.grad is None:
-                    p.grad = g.clone()
-                else:
-                    p.grad.copy_(g)
-                off += n
         self.last_events = self.events
         self.reset()
 
@@ -187,3 +243,4 @@ class GradAllReducer:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        _ACTIVE.discard(self)

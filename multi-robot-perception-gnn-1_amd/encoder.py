@@ -21,6 +21,7 @@ instead of five torch launches.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import weakref
 
@@ -185,13 +186,21 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
     return s
 
 
-def encoder_backward_reductions(dz, dh, h, pose):
+def _grad_out(param, shape, dev):
+    """The gradient buffer of ``param``: its slot in a gradient all-reducer's bucket when one holds
+    it (``dist.grad_out_like``: written in place, adopted by autograd without a copy), else new."""
+    from .dist import grad_out_like
+    g = grad_out_like(param) if param is not None else None
+    return g if g is not None else torch.empty(shape, device=dev)
+
+
+def encoder_backward_reductions(dz, dh, h, pose, b2=None, w1=None, b1=None):
     """(db2 (2C,), dw1 (C, 9), db1 (C,)) via ``mrp_edge_encoder_bwd`` (see module docstring)."""
     E, C = h.shape
     dev = h.device
-    db2 = torch.empty(2 * C, device=dev)
-    dw1 = torch.empty(C, 9, device=dev)
-    db1 = torch.empty(C, device=dev)
+    db2 = _grad_out(b2, (2 * C,), dev)
+    dw1 = _grad_out(w1, (C, 9), dev)
+    db1 = _grad_out(b1, (C,), dev)
     lib = _lib.load_library()
     ws = torch.empty(max(int(lib.mrp_edge_encoder_bwd_workspace(E, C)) // 4, 1), device=dev)
     with torch.cuda.device(dev):
@@ -209,21 +218,22 @@ class EdgeEncoderFunction(torch.autograd.Function):
         pose = pose.contiguous().float()
         h = hidden_forward(pose, w1, b1)
         z = logits_forward(h, w2, b2)
-        ctx.save_for_backward(pose, w1, w2, h)
+        ctx.save_for_backward(pose, w1, w2, h, b1, b2)
         return z
 
     @staticmethod
     def backward(ctx, dz):
-        pose, w1, w2, h = ctx.saved_tensors
+        pose, w1, w2, h, b1, b2 = ctx.saved_tensors
         dz = dz.contiguous()
         need = ctx.needs_input_grad
         cur = torch.cuda.current_stream(dz.device)
         dw2 = None
         if need[3]:
+            dw2 = _grad_out(w2, tuple(w2.shape), dz.device)
             side = _side_stream(dz.device)
             side.wait_stream(cur)
             with torch.cuda.stream(side):  # dW2 = dz^T h beside dh = dz W2
-                dw2 = dz.t().mm(h)
+                torch.mm(dz.t(), h, out=dw2)
             dz.record_stream(side)
             h.record_stream(side)
         dh = dz.mm(w2) if (need[0] or need[1] or need[2]) else None
@@ -232,10 +242,17 @@ class EdgeEncoderFunction(torch.autograd.Function):
             dw2.record_stream(cur)
         db2 = dw1 = db1 = None
         if dh is not None or need[4]:
-            db2, dw1, db1 = encoder_backward_reductions(dz, dh if dh is not None else dz[:, : h.shape[1]], h, pose)
+            db2, dw1, db1 = encoder_backward_reductions(dz, dh if dh is not None else dz[:, : h.shape[1]], h, pose,
+                                                        b2 if need[4] else None, w1 if need[1] else None,
+                                                        b1 if need[2] else None)
         dpose = (dh * (h > 0)).mm(w1) if need[0] else None
         return (dpose, dw1 if need[1] else None, db1 if need[2] else None, dw2,
                 db2 if need[4] else None)
+
+
+#: calls per encoder path ("split": mrp_edge_encoder_fwd_split, "fused": mrp_edge_encoder_fwd,
+#: "autograd": EdgeEncoderFunction) — lets tests assert which kernels a forward actually ran
+PATH_COUNTS = collections.Counter()
 
 
 def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Tensor:
@@ -249,9 +266,12 @@ def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Te
     if _LOGITS_PATH == "split" and inference:
         z = encoder_forward_split(pose, l1, l2)
         if z is not None:
+            PATH_COUNTS["split"] += 1
             return z
     if _LOGITS_PATH == "fused" and inference:
         z = encoder_forward_fused(*params)
         if z is not None:
+            PATH_COUNTS["fused"] += 1
             return z
+    PATH_COUNTS["autograd"] += 1
     return EdgeEncoderFunction.apply(*params)

@@ -38,7 +38,32 @@ from .compress import compress_1x1, compress_path, film_compress, film_compress_
 from .encoder import edge_logits
 
 
-class edge_encoder(nn.Module):  # noqa: N801  (reference class name)
+def clear_packed_weights() -> None:
+    """Drop every cached split-bf16 weight image (edge encoder and 1x1 compress).  The images are
+    keyed by a weight's data pointer and autograd version, which in-place optimizer steps bump;
+    writes that bypass the version counter (``param.data = t``, ``.data`` copies, collectives
+    writing into parameters) need this call.  The modules below call it themselves when they are
+    moved or cast (``.to()``, ``.cuda()``, ``.float()``: ``nn.Module._apply``) and after
+    ``load_state_dict``."""
+    from . import compress, encoder
+    compress.clear_packed_weights()
+    encoder.clear_packed_weights()
+
+
+class _PackedImages:
+    """Mixin: invalidate the packed weight images when parameters are replaced wholesale."""
+
+    def _apply(self, fn, *args, **kwargs):
+        clear_packed_weights()
+        return super()._apply(fn, *args, **kwargs)
+
+    def load_state_dict(self, *args, **kwargs):
+        out = super().load_state_dict(*args, **kwargs)
+        clear_packed_weights()
+        return out
+
+
+class edge_encoder(_PackedImages, nn.Module):  # noqa: N801  (reference class name)
     """FiLM parameter generator, ``dgl/model/models.py:142-155``."""
 
     def __init__(self, layers_dim):
@@ -52,9 +77,10 @@ class edge_encoder(nn.Module):  # noqa: N801  (reference class name)
         )
 
     def logits(self, edge: torch.Tensor) -> torch.Tensor:
-        """Pre-sigmoid FiLM parameters z, (E, C, 2) interleaved.  On the GPU: the hidden layer is a
-        HIP kernel and the second Linear a library GEMM (``encoder.edge_logits``); the sigmoid is
-        left to the aggregation kernel (``MRP_AGG_GB_LOGITS``)."""
+        """Pre-sigmoid FiLM parameters z, (E, C, 2) interleaved.  On the GPU (``encoder.edge_logits``):
+        without a gradient, one split-bf16 matrix-core kernel for both Linears
+        (``mrp_edge_encoder_fwd_split``); with one, HIP kernels that keep the hidden layer for the
+        backward.  The sigmoid is left to the aggregation kernel (``MRP_AGG_GB_LOGITS``)."""
         if edge.is_cuda:
             z = edge_logits(self.layers, edge)
         else:
@@ -80,7 +106,7 @@ def _opt(opt, name, default):
 UNPICKLED_GCN_RETURN = "input"
 
 
-class GCN(nn.Module):
+class GCN(_PackedImages, nn.Module):
     """FiLM-mean graph convolution over per-frame robot graphs, ``dgl/model/models.py:213-226``."""
 
     def __init__(self, opt):
@@ -239,7 +265,7 @@ def _run_stack(module: nn.Module, g, h: torch.Tensor) -> torch.Tensor:
     return h
 
 
-class GCNStack(nn.Module):
+class GCNStack(_PackedImages, nn.Module):
     """k stacked GCN layers (``dgl/model/models.py:162-171,180-189`` generalised; see
     :func:`stack_layout`).  ``state_dict`` keys ``gcn1.*``, ``conv1.*``, ..., ``gcn<k>.*``,
     ``conv<k>.*`` — the reference's naming for k = 1, 2."""
@@ -264,7 +290,7 @@ class GCNBlock(GCNStack):
         super().__init__(opt)
 
 
-class multi_view_dgl_model(nn.Module):  # noqa: N801  (reference class name)
+class multi_view_dgl_model(_PackedImages, nn.Module):  # noqa: N801  (reference class name)
     """``dgl/model/models.py:157-205`` with caller-supplied CNN ``encoder``/``decoder``.
 
     ``encoder(images (B, N, 3, S, S)) -> list of feature maps`` (last one used) and

@@ -262,3 +262,105 @@ def _empty_shard_worker(rank, world, port):
 
 def test_grad_allreduce_world2_batch1_empty_shard():
     mp.spawn(_empty_shard_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+class _MatW(torch.autograd.Function):
+    """y = x W^T whose weight gradient is written where ``dist.grad_out_like`` says (as the HIP
+    backward kernels do): into the reducer's bucket slot."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x.mm(w.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        from mrp_gnn_amd.dist import grad_out_like
+        x, w = ctx.saved_tensors
+        dw = grad_out_like(w)
+        if dw is None:
+            dw = torch.empty_like(w)
+        torch.mm(gy.t(), x, out=dw)
+        return gy.mm(w), dw
+
+
+def _views_worker(rank, world, port):
+    """Gradients live in the reducer's flat buckets (p.grad are views of them): no per-step
+    concatenation or copy back; a gradient written through grad_out_like is adopted with no copy at
+    all; one autograd allocated is copied into its slot once; zero_grad(set_to_none=False)
+    accumulates straight into the views (no copy).  Results equal the full-batch gradients."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(7)
+        data, target = torch.randn(8, 9), torch.randn(8, 5)
+        w_ref = torch.randn(5, 9)
+        lin_ref = torch.nn.Linear(9, 9)
+        ref_w = w_ref.clone().requires_grad_(True)
+        lin_r = torch.nn.Linear(9, 9)
+        lin_r.load_state_dict(lin_ref.state_dict())
+        torch.nn.functional.mse_loss(_MatW.apply(lin_r(data), ref_w), target).backward()
+        w = torch.nn.Parameter(w_ref.clone())
+        lin = torch.nn.Linear(9, 9)
+        lin.load_state_dict(lin_ref.state_dict())
+        params = [w] + list(lin.parameters())
+        red = GradAllReducer(params, bucket_bytes=1 << 20)
+        assert len(red.buckets) == 1
+        flat = red._flat[0]
+        lo, hi = shard_range(8, rank, world)
+
+        def in_bucket(t):
+            base = flat.data_ptr()
+            return base <= t.data_ptr() < base + flat.numel() * flat.element_size()
+
+        for step in range(3):
+            before = red.copies
+            if step < 2:
+                for p in params:
+                    p.grad = None
+            else:
+                for p in params:
+                    p.grad.zero_()  # zero_grad(set_to_none=False): accumulate into the views
+            torch.nn.functional.mse_loss(_MatW.apply(lin(data[lo:hi]), w), target[lo:hi]).backward()
+            red.synchronize()
+            copies = red.copies - before
+            # the Linear's two gradients are allocated by autograd (copied once each) unless they
+            # already are the views; w's is written in its slot by the backward itself
+            assert copies == (2 if step < 2 else 0), (step, copies)
+            for p in params:
+                assert in_bucket(p.grad), step
+            assert torch.allclose(w.grad, ref_w.grad, rtol=1e-5, atol=1e-6)
+            for p, q in zip(lin.parameters(), lin_r.parameters()):
+                assert torch.allclose(p.grad, q.grad, rtol=1e-5, atol=1e-6)
+        red.remove()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_bucket_views_world2():
+    mp.spawn(_views_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def test_bench_self_launch_command():
+    """bench.py --gpus N (no launcher around it) starts N ranks itself: torch.distributed.run on
+    127.0.0.1, one process per GPU, the same arguments, WORLD_SIZE left to the launcher."""
+    import importlib.util
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    os.environ["WORLD_SIZE"] = "3"
+    try:
+        cmd, env = bench.launcher_command(["--gpus", "4", "--steps", "5"], 4, 29555)
+    finally:
+        del os.environ["WORLD_SIZE"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--master-port=29555" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-3:] == ["--gpus", "4", "--steps", "5"][-3:] and cmd[-4] == "--gpus"
+    assert os.path.basename(cmd[cmd.index("--master-port=29555") + 1]) == "bench.py"
+    assert "WORLD_SIZE" not in env and env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    args = bench.parse_args(["--gpus", "2", "--dist-backend", "gloo"])
+    assert args.gpus == 2 and args.dist_backend == "gloo"
