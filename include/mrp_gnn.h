@@ -381,8 +381,9 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * (mrp_edge_encoder_fwd tile/buffer variant, 0..4); "edge_split_cb" (mrp_edge_encoder_fwd_split: 32-column
  * blocks per wave, 1 or 2; 0, default: per shape); "edge_split_k" (its hidden blocks over 1 or 2
  * wave sets, 2 only when C % 64 == 0; 0, default: per shape); "gemm_split" (split-bf16 compress
- * forward / data-gradient kernel: -1 per shape, 2 = 128 rows / 4 waves, 4 = 256 rows / 8 waves with
- * 32-k stages, 5 = 256 rows / 8 waves, pipelined 16-k stages; any other value is rejected). */
+ * forward / data-gradient kernel: -1 per shape (5 where M % 256 == 0, else 2), 2 = 128 rows / 4 waves,
+ * 4 = 256 rows / 8 waves with 32-k stages, 5 = 256 rows / 8 waves, pipelined 16-k stages, 6 = two
+ * pipelined 128-row / 4-wave workgroups per CU; any other value is rejected). */
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 16 = this header: v15 plus

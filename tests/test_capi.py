@@ -156,17 +156,17 @@ def test_tuning_knobs_documented_in_the_header():
         for name, lo, hi in (("bwd_regular_mfma", 0, 1), ("bwd_complete_mfma", 0, 1), ("bwd_mfma_cpw", 1, 2),
                              ("bwd_pre2", 0, 1), ("fwd_regular_split", 0, 1), ("bwd_fused_cap", 1, 64),
                              ("gemm_nn", -1, 5), ("gemm_nt", -1, 5), ("edge_gemm", 0, 1), ("edge_fused", 0, 4),
-                             ("edge_split_cb", 0, 2), ("edge_split_k", 0, 2), ("gemm_split", -1, 5)):
+                             ("edge_split_cb", 0, 2), ("edge_split_k", 0, 2), ("gemm_split", -1, 6)):
             assert name.encode() in open(os.path.join(ROOT, "include", "mrp_gnn.h"), "rb").read() or \
                 name.startswith("bwd_fused")
             assert lib.mrp_tuning_set(name.encode(), lo) == 0
             assert lib.mrp_tuning_set(name.encode(), hi) == 0
             assert lib.mrp_tuning_set(name.encode(), hi + 1) == HIP_INVALID_VALUE
         assert lib.mrp_tuning_set(b"no_such_knob", 0) == HIP_INVALID_VALUE
-        # gemm_split names a kernel (-1 per shape, 2, 4, 5): the values between name none
+        # gemm_split names a kernel (-1 per shape, 2, 4, 5, 6): the values between name none
         for v in (0, 1, 3):
             assert lib.mrp_tuning_set(b"gemm_split", v) == HIP_INVALID_VALUE
-        for v in (-1, 2, 4, 5):
+        for v in (-1, 2, 4, 5, 6):
             assert lib.mrp_tuning_set(b"gemm_split", v) == 0
     finally:
         assert lib.mrp_tuning_set(b"reset", 0) == 0
