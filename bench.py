@@ -94,10 +94,11 @@ def alg_bytes_fwd(Nt, E, C, P):
     return Nt * C * P * 4 + E * 2 * C * 4 + Nt * C * P * 4
 
 
-def alg_bytes_bwd(Nt, E, C, P):
+def alg_bytes_bwd(Nt, E, C, P, base=False):
     """Backward (dx + d gamma/beta): grad_out and x read once, gamma/beta read once, dx written once,
-    d gamma/beta written once."""
-    return 2 * Nt * C * P * 4 + E * 2 * C * 4 + Nt * C * P * 4 + E * 2 * C * 4
+    d gamma/beta written once; ``base``: the training form, which also reads the
+    grad_x base (x's gradient from the 1x1 compress, added into dx) once."""
+    return (3 if base else 2) * Nt * C * P * 4 + E * 2 * C * 4 + Nt * C * P * 4 + E * 2 * C * 4
 
 
 def time_launches(launches, iters, device):
@@ -456,18 +457,25 @@ def config_record(cid, world, rank, device, args):
     rec["roofline_fwd"] = roofline(kname, alg_bytes_fwd(Nt, E, C, P), tf, rotating_sets=nf,
                                    footprint_mb=round(nf * (2 * plane) / 2**20))
     del sets, launches
-    nb = rotating_sets(3 * plane + 2 * E * 2 * C * 4)
-    bsets = [(torch.randn_like(x), x if i == 0 else torch.randn_like(x)) for i in range(nb)]
+    # the backward as training runs it (FilmCompressFunction: x's compress gradient is the base that
+    # the kernel adds into dx, the DXB instantiation), and without the base for comparison
+    nb = rotating_sets(4 * plane + 2 * E * 2 * C * 4)
+    bsets = [(torch.randn_like(x), x if i == 0 else torch.randn_like(x), torch.randn_like(x)) for i in range(nb)]
 
-    def bwd(G, xi):
-        return mrp.aggregate.film_mean_backward(G, xi, z, csr, mode, True, True)
+    def bwd(G, xi, base):
+        return mrp.aggregate.film_mean_backward(G, xi, z, csr, mode, True, True, grad_x_base=base)
 
-    launches = [lambda G=G, xi=xi: bwd(G, xi) for G, xi in bsets]
-    tb = time_launches(launches, args.kernel_iters, device)
     # k-NN graphs of > 8 nodes: the matrix-core backward (whole 64-pixel groups), else the VALU kernels
     bname = (("film_bwd_mfma" if P % 64 == 0 else "film_bwd_regular") if knn and N > 8 else "film_bwd_fused")
-    rec["roofline_bwd"] = roofline(bname, alg_bytes_bwd(Nt, E, C, P), tb, rotating_sets=nb,
-                                   footprint_mb=round(nb * (3 * plane) / 2**20))
+    launches = [lambda G=G, xi=xi, bs=bs: bwd(G, xi, bs) for G, xi, bs in bsets]
+    tb = time_launches(launches, args.kernel_iters, device)
+    rec["roofline_bwd"] = roofline(bname, alg_bytes_bwd(Nt, E, C, P, base=True), tb, rotating_sets=nb,
+                                   footprint_mb=round(nb * (4 * plane) / 2**20),
+                                   form="training: grad_x base added in-kernel (the DXB instantiation)")
+    launches = [lambda G=G, xi=xi: bwd(G, xi, None) for G, xi, _ in bsets]
+    tb0 = time_launches(launches, args.kernel_iters, device)
+    rec["roofline_bwd_no_base"] = roofline(bname, alg_bytes_bwd(Nt, E, C, P), tb0, rotating_sets=nb,
+                                           footprint_mb=round(nb * (3 * plane) / 2**20))
     del bsets, launches
     return rec
 

@@ -334,6 +334,39 @@ int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const floa
                                float* z, void* stream);
 
 /*
+ * The encoder's training path on the split-bf16 matrix cores (replaces mrp_edge_hidden_fwd +
+ * mrp_edge_logits_fwd forward and the two library GEMMs of the backward, dgl/model/models.py:146-149
+ * under dgl/training.py:208-210's loss.backward()):
+ *   mrp_edge_encoder_fwd_split_train   as mrp_edge_encoder_fwd_split (shared-hidden form), and also
+ *                                      h^T = relu(pose W1^T + b1)^T, (C, E) rows of hT_stride >= E floats
+ *   mrp_edge_encoder_bwd_prep          dzT (2C, E) rows of dzT_stride >= E = dz^T (E % 4 == 0, C even,
+ *                                      16-byte aligned, dzT_stride % 4 == 0; else hipErrorNotSupported)
+ *   mrp_edge_encoder_bwd_split         dh^T (C, E) = W2^T dz^T and dW2 (2C, C) = dz^T h on the split-bf16
+ *                                      weight-gradient kernel (either output may be NULL), with db2 (2C) =
+ *                                      column sums of dz taken on the dW2 product (NULL, or dw2 non-NULL);
+ *                                      w2T = W2^T (C, 2C) row-major; dzT and hT with row stride E;
+ *                                      workspace: _split_workspace(E, C) bytes (0 if none is needed) —
+ *                                      the two products may be issued as two calls on two streams, each
+ *                                      with its own workspace
+ *   mrp_edge_encoder_bwd_t             dpre = dh^T (.) [h^T > 0]: dw1 (C, 9) = dpre pose, db1 (C) = row sums
+ *                                      (either may be NULL); workspace: _t_workspace(E, C) bytes
+ * Requirements of _bwd_split (else hipErrorNotSupported): E % 32 == 0, C % 32 == 0, 16-byte aligned
+ * operands.  All sums in a fixed order: deterministic.
+ */
+int mrp_edge_encoder_fwd_split_train(const float* pose, const void* packed, const float* b2, int32_t num_edges,
+                                     int32_t C, float* z, float* hT, int64_t hT_stride, void* stream);
+int mrp_edge_encoder_bwd_prep(const float* dz, int32_t num_edges, int32_t C, float* dzT, int64_t dzT_stride,
+                              void* stream);
+int64_t mrp_edge_encoder_bwd_split_workspace(int32_t num_edges, int32_t C);
+int mrp_edge_encoder_bwd_split(const float* dz, const float* dzT, const float* w2T, const float* hT,
+                               int32_t num_edges, int32_t C, float* dhT, float* dw2, float* db2, void* workspace,
+                               int64_t workspace_bytes, void* stream);
+int64_t mrp_edge_encoder_bwd_t_workspace(int32_t num_edges, int32_t C);
+int mrp_edge_encoder_bwd_t(const float* dhT, int64_t dhT_stride, const float* hT, int64_t hT_stride,
+                           const float* pose, int32_t num_edges, int32_t C, float* dw1, float* db1, void* workspace,
+                           int64_t workspace_bytes, void* stream);
+
+/*
  * Backward of the edge encoder's reductions (dgl/model/models.py:147-149), run after the two
  * library GEMMs of its backward (dh = dz W2, dW2 = dz^T h):
  *   db2[j]    = sum_e dz[e, j]                              (dz: (E, 2C), the logits' gradient that
@@ -375,10 +408,12 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * "bwd_fused_*", "bwd_regular_*"; kernel choice: "bwd_regular_mfma" (1, default: the matrix-core
  * backward for MRP_GRAPH_REGULAR graphs of 9..16 nodes), "bwd_complete_mfma" (1, default: the
  * matrix-core backward for complete graphs of 9..16 nodes too; those of <= 8 always run the VALU one), "bwd_mfma_cpw" (channel blocks per wave of the matrix-core
- * backward, 1 or 2), "bwd_pre2", "fwd_regular_split" (0, default: whole planes); compress GEMM
+ * backward, 1 or 2), "bwd_pre2" (0 off, 1 on, 2 on unless a grad_x base is given), "fwd_regular_split" (0, default: whole planes); compress GEMM
  * kernel variants "gemm_nn" / "gemm_nt" (-1, default: the per-shape choice; 0..5: compress_gemm.hip's
  * variant table); "edge_gemm" (1, default: mrp_edge_logits_fwd on 32x32x2 MFMAs; 0: 16x16x4); "edge_fused"
- * (mrp_edge_encoder_fwd tile/buffer variant, 0..4); "edge_split_cb" (mrp_edge_encoder_fwd_split: 32-column
+ * (mrp_edge_encoder_fwd tile/buffer variant, 0..4); "edge_split_v" (mrp_edge_encoder_fwd_split form: -1,
+ * default: per shape; 0: the per-wave hidden layer; 1..4: the hidden layer shared by a workgroup of 4
+ * or 8 waves with 1 or 2 column blocks each); "edge_split_cb" (form 0: 32-column
  * blocks per wave, 1 or 2; 0, default: per shape); "edge_split_k" (its hidden blocks over 1 or 2
  * wave sets, 2 only when C % 64 == 0; 0, default: per shape); "gemm_split" (split-bf16 compress
  * forward / data-gradient kernel: -1 per shape (5 where M % 256 == 0, else 2), 2 = 128 rows / 4 waves,
@@ -386,7 +421,9 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * pipelined 128-row / 4-wave workgroups per CU; any other value is rejected). */
 int mrp_tuning_set(const char* name, int32_t value);
 
-/* Library identification: ABI version (incremented on signature changes; 16 = this header: v15 plus
+/* Library identification: ABI version (incremented on signature changes; 17 = this header: v16 plus
+ * the split-bf16 training path of the edge encoder (mrp_edge_encoder_fwd_split_train, _bwd_prep,
+ * _bwd_split, _bwd_t and their workspaces); 16: v15 plus
  * the split-bf16 weight gradient (mrp_compress_bwd_weight_split + workspace); 15: v14 plus
  * the split-bf16 compress forward / data gradient and their weight packing (mrp_compress_split_*,
  * mrp_compress_fwd_split, mrp_compress_bwd_data_split); 14: v13 plus

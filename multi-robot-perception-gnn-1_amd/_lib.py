@@ -42,14 +42,20 @@ EXPORTED_SYMBOLS = (
     "mrp_edge_encoder_pack_bytes",
     "mrp_edge_encoder_pack",
     "mrp_edge_encoder_fwd_split",
+    "mrp_edge_encoder_fwd_split_train",
     "mrp_edge_encoder_bwd_workspace",
     "mrp_edge_encoder_bwd",
+    "mrp_edge_encoder_bwd_prep",
+    "mrp_edge_encoder_bwd_split_workspace",
+    "mrp_edge_encoder_bwd_split",
+    "mrp_edge_encoder_bwd_t_workspace",
+    "mrp_edge_encoder_bwd_t",
     "mrp_frame_graph_build",
     "mrp_tuning_set",
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 16
+ABI_VERSION = 17
 MAX_NODES = 16
 
 HIP_ERROR_NOT_SUPPORTED = 801  # hipErrorNotSupported: a fused path declines this shape
@@ -138,6 +144,18 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_edge_encoder_pack.restype = ctypes.c_int
     lib.mrp_edge_encoder_fwd_split.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_encoder_fwd_split.restype = ctypes.c_int
+    lib.mrp_edge_encoder_fwd_split_train.argtypes = [_P, _P, _P, _I32, _I32, _P, _P, _I64, _P]
+    lib.mrp_edge_encoder_fwd_split_train.restype = ctypes.c_int
+    lib.mrp_edge_encoder_bwd_prep.argtypes = [_P, _I32, _I32, _P, _I64, _P]
+    lib.mrp_edge_encoder_bwd_prep.restype = ctypes.c_int
+    lib.mrp_edge_encoder_bwd_split_workspace.argtypes = [_I32, _I32]
+    lib.mrp_edge_encoder_bwd_split_workspace.restype = ctypes.c_int64
+    lib.mrp_edge_encoder_bwd_split.argtypes = [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _I64, _P]
+    lib.mrp_edge_encoder_bwd_split.restype = ctypes.c_int
+    lib.mrp_edge_encoder_bwd_t_workspace.argtypes = [_I32, _I32]
+    lib.mrp_edge_encoder_bwd_t_workspace.restype = ctypes.c_int64
+    lib.mrp_edge_encoder_bwd_t.argtypes = [_P, _I64, _P, _I64, _P, _I32, _I32, _P, _P, _P, _I64, _P]
+    lib.mrp_edge_encoder_bwd_t.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]
     lib.mrp_edge_encoder_bwd_workspace.restype = ctypes.c_int64
     lib.mrp_edge_encoder_bwd.argtypes = [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P]

@@ -876,8 +876,9 @@ int nt_splits(int64_t tiles, int64_t ktot, int64_t M, int64_t N, int64_t* kchunk
     const int64_t per = (stages + s - 1) / s;
     if ((stages + per - 1) / per != s) continue;  // some split would be empty
     const int64_t rounds = (tiles * s + 255) / 256;
-    // one stage of a 256 x 128 workgroup at ~190 TF/s-equivalent: ~0.09 us
-    const double cost = (double)rounds * per * 0.09 + (s > 1 ? (double)M * N * 4.0 * (s + 1) / 4.0e6 + 4.0 : 0.0);
+    // one 32-k stage of a 256 x 128 workgroup (12.6 MFLOP of bf16 products on one CU, ~1.3 us at the
+    // CU's peak) takes ~1.6 us; the split sum streams the partial tiles at ~4 TB/s plus a launch
+    const double cost = (double)rounds * per * 1.6 + (s > 1 ? (double)M * N * 4.0 * (s + 1) / 4.0e6 + 4.0 : 0.0);
     if (cost < best_cost) {
       best_cost = cost;
       best = s;
@@ -973,15 +974,50 @@ namespace {
 bool nt_split_ok(int32_t num_nodes, int32_t C, int32_t P) {
   return num_nodes > 0 && C > 0 && C % 64 == 0 && P % BK == 0;
 }
+
+// workspace bytes of one NT product (split-K partial tiles, and row sums when wanted)
+int64_t nt_workspace(int64_t M, int64_t N, int64_t ktot) {
+  const int64_t tiles = ((M + NTGeo<4>::TM - 1) / NTGeo<4>::TM) * ((N + TN - 1) / TN);
+  int64_t kchunk;
+  const int ns = nt_splits(tiles, ktot, M, N, &kchunk);
+  return ns <= 1 ? 0 : ((int64_t)ns * M * N + (int64_t)ns * M) * 4;
+}
+
+// out (M x N) = sum_k g[m][k] s[n][k] (+ row sums of g into outb), k = (node, pixel) over `nodes` nodes of
+// P pixels; a.g/gs, a.s0/s0s, a.s1/s1s, a.n0, a.P set by the caller
+hipError_t nt_run(NTArgs a, int64_t M, int64_t N, int32_t nodes, float* out, float* outb, void* workspace,
+                  int64_t workspace_bytes, hipStream_t st) {
+  using G = NTGeo<4>;
+  a.mtiles = (int32_t)((M + G::TM - 1) / G::TM);
+  a.ntiles = (int32_t)((N + TN - 1) / TN);
+  a.ktot = (int64_t)nodes * a.P;
+  const int ns = nt_splits((int64_t)a.mtiles * a.ntiles, a.ktot, M, N, &a.kchunk);
+  const int64_t need = ns == 1 ? 0 : ((int64_t)ns * M * N + (int64_t)ns * M) * 4;
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need || !aligned16(workspace))) return hipErrorInvalidValue;
+  float* ws = static_cast<float*>(workspace);
+  a.out = ns == 1 ? out : ws;
+  a.outb = outb == nullptr ? nullptr : (ns == 1 ? outb : ws + (int64_t)ns * M * N);
+  a.M = (int32_t)M;
+  a.N = (int32_t)N;
+  const int64_t grid = (int64_t)a.mtiles * a.ntiles * ns;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split_w4),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(gemm_nt_split_w4, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || ns == 1) return e;
+  const int64_t n4 = M * N / 4;
+  const int64_t blocks = (n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048;
+  hipLaunchKernelGGL(split_sum_nt, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<const f4*>(ws), ns, n4,
+                     reinterpret_cast<f4*>(out), a.outb, (int32_t)M, outb);
+  return hipGetLastError();
+}
 }  // namespace
 
 extern "C" int64_t mrp_compress_bwd_weight_split_workspace(int32_t num_nodes, int32_t C, int32_t P) {
   if (!nt_split_ok(num_nodes, C, P)) return 0;
-  const int64_t M = C, N = 2 * (int64_t)C;
-  const int64_t tiles = ((M + NTGeo<4>::TM - 1) / NTGeo<4>::TM) * ((N + TN - 1) / TN);
-  int64_t kchunk;
-  const int ns = nt_splits(tiles, (int64_t)num_nodes * P, M, N, &kchunk);
-  return ns <= 1 ? 0 : ((int64_t)ns * M * N + (int64_t)ns * M) * 4;
+  return nt_workspace(C, 2 * (int64_t)C, (int64_t)num_nodes * P);
 }
 
 extern "C" int mrp_compress_bwd_weight_split(const float* gy, int64_t gy_node_stride, const float* x,
@@ -1004,38 +1040,64 @@ extern "C" int mrp_compress_bwd_weight_split(const float* gy, int64_t gy_node_st
   if (!nt_split_ok(num_nodes, C, P) || (gy_node_stride & 3) || (x_node_stride & 3) || (agg_node_stride & 3) ||
       !aligned16(gy) || !aligned16(x) || !aligned16(agg) || !aligned16(gw))
     return hipErrorNotSupported;
-  using G = NTGeo<4>;
   NTArgs a = {};
-  a.mtiles = (int32_t)((M + G::TM - 1) / G::TM);
-  a.ntiles = (int32_t)((N + TN - 1) / TN);
-  a.ktot = (int64_t)num_nodes * P;
-  const int ns = nt_splits((int64_t)a.mtiles * a.ntiles, a.ktot, M, N, &a.kchunk);
-  const int64_t need = ns == 1 ? 0 : ((int64_t)ns * M * N + (int64_t)ns * M) * 4;
-  if (need > 0 && (workspace == nullptr || workspace_bytes < need || !aligned16(workspace))) return hipErrorInvalidValue;
-  float* ws = static_cast<float*>(workspace);
   a.g = gy;
   a.gs = gy_node_stride;
   a.s0 = x;
   a.s0s = x_node_stride;
   a.s1 = agg;
   a.s1s = agg_node_stride;
-  a.out = ns == 1 ? gw : ws;
-  a.outb = gbias == nullptr ? nullptr : (ns == 1 ? gbias : ws + (int64_t)ns * M * N);
-  a.M = (int32_t)M;
-  a.N = (int32_t)N;
   a.n0 = C;
   a.P = P;
-  const int64_t grid = (int64_t)a.mtiles * a.ntiles * ns;
-  if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split_w4),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
-  if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL(gemm_nt_split_w4, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || ns == 1) return e;
-  const int64_t n4 = M * N / 4;
-  const int64_t blocks = (n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048;
-  hipLaunchKernelGGL(split_sum_nt, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<const f4*>(ws), ns, n4,
-                     reinterpret_cast<f4*>(gw), a.outb, (int32_t)M, gbias);
-  return hipGetLastError();
+  return nt_run(a, M, N, num_nodes, gw, gbias, workspace, workspace_bytes, st);
+}
+
+// The edge encoder's backward GEMMs on the same kernel (training path, encoder.py): operands are rows
+// with k contiguous, i.e. one "node" of K pixels:
+//   dh^T (C x E)  = W2^T (C x 2C) . dz^T     (k = j: rows of W2^T and of dz)
+//   dW2 (2C x C)  = dz^T (2C x E) . h         (k = e: rows of dz^T and of h^T; db2 = its row sums of dz^T)
+extern "C" int64_t mrp_edge_encoder_bwd_split_workspace(int32_t num_edges, int32_t C) {
+  if (num_edges <= 0 || C <= 0 || num_edges % BK != 0 || C % 32 != 0) return 0;
+  const int64_t a = nt_workspace(C, num_edges, 2 * (int64_t)C), b = nt_workspace(2 * (int64_t)C, C, num_edges);
+  return a > b ? a : b;
+}
+
+extern "C" int mrp_edge_encoder_bwd_split(const float* dz, const float* dzT, const float* w2T, const float* hT,
+                                          int32_t num_edges, int32_t C, float* dhT, float* dw2, float* db2,
+                                          void* workspace, int64_t workspace_bytes, void* stream) {
+  if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
+  if (db2 != nullptr && dw2 == nullptr) return hipErrorInvalidValue;  // db2 rides on the dW2 product
+  if (num_edges == 0 || C == 0 || (dhT == nullptr && dw2 == nullptr)) return hipSuccess;
+  if (num_edges % BK != 0 || C % 32 != 0) return hipErrorNotSupported;
+  if ((dhT && (!dz || !w2T || !aligned16(dz) || !aligned16(w2T) || !aligned16(dhT))) ||
+      (dw2 && (!dzT || !hT || !aligned16(dzT) || !aligned16(hT) || !aligned16(dw2))))
+    return hipErrorInvalidValue;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t E = num_edges, C2 = 2 * (int64_t)C;
+  if (dhT) {
+    NTArgs a = {};
+    a.g = w2T;  // rows u, k = j
+    a.gs = C * C2;
+    a.s0 = dz;  // rows e, k = j
+    a.s0s = E * C2;
+    a.s1 = dz;
+    a.s1s = E * C2;
+    a.n0 = (int32_t)E;
+    a.P = (int32_t)C2;
+    const hipError_t e = nt_run(a, C, E, 1, dhT, nullptr, workspace, workspace_bytes, st);
+    if (e != hipSuccess) return e;
+  }
+  if (dw2) {
+    NTArgs a = {};
+    a.g = dzT;  // rows j, k = e
+    a.gs = C2 * E;
+    a.s0 = hT;  // rows u, k = e
+    a.s0s = (int64_t)C * E;
+    a.s1 = hT;
+    a.s1s = (int64_t)C * E;
+    a.n0 = C;
+    a.P = (int32_t)E;
+    return nt_run(a, C2, C, 1, dw2, db2, workspace, workspace_bytes, st);  // row sums of dz^T = db2
+  }
+  return hipSuccess;
 }

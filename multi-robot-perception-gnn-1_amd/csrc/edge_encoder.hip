@@ -192,3 +192,155 @@ extern "C" int mrp_edge_encoder_bwd(const float* dz, const float* dh, const floa
                      db2, dw1, db1);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------
+// Backward in the transposed layout of the split-bf16 training path (encoder.py, EdgeEncoderSplitFunction):
+// the forward wrote h^T (C, E); the two GEMMs dh^T = W2^T dz^T and dW2 = dz^T h run on the split-bf16
+// weight-gradient kernel (compress_split.hip, mrp_edge_encoder_bwd_split, which also takes db2 as the
+// row sums of dz^T), whose operands are rows with k contiguous — so dz is first transposed:
+//   mrp_edge_encoder_bwd_prep:  dzT[j][e] = dz[e][j]
+//   mrp_edge_encoder_bwd_t:     dpre = dh^T (.) [h^T > 0];  dw1[k][i] = sum_e dpre[k][e] pose[e][i],
+//                               db1[k] = sum_e dpre[k][e]
+// The e sums run per 256-edge block (fixed lane order, fixed butterfly) into partials summed over the
+// blocks in order by a second pass: deterministic.
+// ------------------------------------------------------------------------------------------------
+namespace mrp_enc {
+
+typedef float f4t __attribute__((ext_vector_type(4)));
+
+// 64 (e) x 64 (j) tile through LDS (+1 padding), 16-byte accesses both ways: thread t moves the 4-float
+// pieces (t & 15) of rows (t >> 4) + 16 i; E % 4 == 0 and N2 % 4 == 0 (checked by the entry point)
+__global__ void __launch_bounds__(256) dz_transpose(const float* __restrict__ dz, int E, int N2,
+                                                    float* __restrict__ dzT, int64_t dzT_stride) {
+  __shared__ float tile[64][65];
+  const int j0 = blockIdx.x * 64, e0 = blockIdx.y * 64;
+  const int c4 = threadIdx.x & 15, r0 = threadIdx.x >> 4;
+  f4t v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = e0 + r0 + 16 * i, j = j0 + 4 * c4;
+    v[i] = (e < E && j < N2) ? *reinterpret_cast<const f4t*>(dz + (int64_t)e * N2 + j) : f4t{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tile[r0 + 16 * i][4 * c4 + q] = v[i][q];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int jr = r0 + 16 * i, j = j0 + jr, e = e0 + 4 * c4;
+    f4t o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = tile[4 * c4 + q][jr];
+    if (j < N2 && e < E) *reinterpret_cast<f4t*>(dzT + (int64_t)j * dzT_stride + e) = o;
+  }
+}
+
+constexpr int BT_E = 256;  // edges per block of encoder_bwd_t
+
+// block (k group of 4, e block): wave w sums unit k = 4 blockIdx.x + w over the block's 256 edges; the
+// block's pose rows are staged in LDS once; partial [e block][k][10] (9 dw1 terms, db1)
+__global__ void __launch_bounds__(256) encoder_bwd_t(const float* __restrict__ dhT, int64_t dhs,
+                                                     const float* __restrict__ hT, int64_t hs,
+                                                     const float* __restrict__ pose, int E, int C,
+                                                     float* __restrict__ part) {
+  __shared__ float ps[BT_E * NIN];
+  const int eb = blockIdx.y, ebase = eb * BT_E;
+  const int nrow = E - ebase < BT_E ? E - ebase : BT_E;
+  for (int i = threadIdx.x; i < nrow * NIN; i += 256) ps[i] = pose[(int64_t)ebase * NIN + i];
+  __syncthreads();
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (k >= C) return;
+  float hv[BT_E / 64], dv[BT_E / 64];
+#pragma unroll
+  for (int it = 0; it < BT_E / 64; ++it) {
+    const int el = lane + 64 * it;
+    hv[it] = el < nrow ? hT[(int64_t)k * hs + ebase + el] : 0.f;
+    dv[it] = el < nrow ? dhT[(int64_t)k * dhs + ebase + el] : 0.f;
+  }
+  float acc[NIN + 1];
+#pragma unroll
+  for (int i = 0; i <= NIN; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int it = 0; it < BT_E / 64; ++it) {
+    const int el = lane + 64 * it;
+    const float d = hv[it] > 0.f ? dv[it] : 0.f;
+    if (el < nrow) {
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) acc[i] = fmaf(d, ps[el * NIN + i], acc[i]);
+    }
+    acc[NIN] += d;
+  }
+#pragma unroll
+  for (int i = 0; i <= NIN; ++i)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc[i] += __shfl_xor(acc[i], o, 64);
+  if (lane <= NIN) {
+    float v = acc[0];
+#pragma unroll
+    for (int i = 1; i <= NIN; ++i) v = lane == i ? acc[i] : v;
+    part[((int64_t)eb * C + k) * (NIN + 1) + lane] = v;
+  }
+}
+
+// (k, i) per thread: the e-block partials summed in block order
+__global__ void __launch_bounds__(256) encoder_bwd_t_final(const float* __restrict__ part, int neb, int C,
+                                                           float* __restrict__ dw1, float* __restrict__ db1) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= C * (NIN + 1)) return;
+  float s = 0.f;
+  for (int b = 0; b < neb; ++b) s += part[(int64_t)b * C * (NIN + 1) + t];
+  const int k = t / (NIN + 1), i = t - k * (NIN + 1);
+  if (i < NIN) {
+    if (dw1 != nullptr) dw1[(int64_t)k * NIN + i] = s;
+  } else if (db1 != nullptr) {
+    db1[k] = s;
+  }
+}
+
+}  // namespace mrp_enc
+
+extern "C" int mrp_edge_encoder_bwd_prep(const float* dz, int32_t num_edges, int32_t C, float* dzT,
+                                         int64_t dzT_stride, void* stream) {
+  if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
+  if (num_edges == 0 || C == 0) return hipSuccess;
+  const int N2 = 2 * C;
+  if (!dz || !dzT || dzT_stride < num_edges) return hipErrorInvalidValue;
+  if (num_edges % 4 != 0 || N2 % 4 != 0 || dzT_stride % 4 != 0 || (reinterpret_cast<uintptr_t>(dz) & 15) ||
+      (reinterpret_cast<uintptr_t>(dzT) & 15))
+    return hipErrorNotSupported;
+  hipLaunchKernelGGL(mrp_enc::dz_transpose, dim3((N2 + 63) / 64, (num_edges + 63) / 64), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), dz, num_edges, N2, dzT, dzT_stride);
+  return hipGetLastError();
+}
+
+extern "C" int64_t mrp_edge_encoder_bwd_t_workspace(int32_t num_edges, int32_t C) {
+  if (num_edges <= 0 || C <= 0) return 0;
+  return (int64_t)((num_edges + mrp_enc::BT_E - 1) / mrp_enc::BT_E) * C * (mrp_enc::NIN + 1) * 4;
+}
+
+extern "C" int mrp_edge_encoder_bwd_t(const float* dhT, int64_t dhT_stride, const float* hT, int64_t hT_stride,
+                                      const float* pose, int32_t num_edges, int32_t C, float* dw1, float* db1,
+                                      void* workspace, int64_t workspace_bytes, void* stream) {
+  if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
+  if (C == 0 || (dw1 == nullptr && db1 == nullptr)) return hipSuccess;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (num_edges == 0) {  // empty sums
+    if (dw1 && hipMemsetAsync(dw1, 0, (size_t)C * mrp_enc::NIN * 4, st) != hipSuccess) return hipErrorUnknown;
+    if (db1 && hipMemsetAsync(db1, 0, (size_t)C * 4, st) != hipSuccess) return hipErrorUnknown;
+    return hipSuccess;
+  }
+  if (!dhT || !hT || !pose || dhT_stride < num_edges || hT_stride < num_edges || !workspace ||
+      workspace_bytes < mrp_edge_encoder_bwd_t_workspace(num_edges, C))
+    return hipErrorInvalidValue;
+  const int neb = (num_edges + mrp_enc::BT_E - 1) / mrp_enc::BT_E;
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(mrp_enc::encoder_bwd_t, dim3((C + 3) / 4, neb), dim3(256), 0, st, dhT, dhT_stride, hT,
+                     hT_stride, pose, num_edges, C, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(mrp_enc::encoder_bwd_t_final, dim3((C * (mrp_enc::NIN + 1) + 255) / 256), dim3(256), 0, st, part, neb, C,
+                     dw1, db1);
+  return hipGetLastError();
+}

@@ -165,6 +165,8 @@ struct FwdArgs {
   const u4* packed;
   const float* b2;
   float* z;
+  float* hT;     // shared-hidden forms, training: relu(pose W1^T + b1) transposed, (C, E) rows of hts floats
+  int64_t hts;
   int32_t E, C, egroups;
 };
 
@@ -407,6 +409,195 @@ hipError_t launch_fwd(int cb, int ks, const FwdArgs& a, int64_t grid, hipStream_
   return cb == 2 ? launch_cfg<2, 1>(encoder_fwd_cb2, a, grid, st) : launch_cfg<1, 1>(encoder_fwd_cb1, a, grid, st);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Shared-hidden form (mrp_edge_encoder_fwd_split's default).  A workgroup's NWV waves share one block
+// of 32 edges and own NWV x CB adjacent 32-column blocks of z.  Per round of NWV hidden blocks, wave w
+// computes X (32 units x 32 edges) of hidden block round NWV + w on the matrix cores, applies the ReLU,
+// splits it and stores its A-operand fragments (6 x 16 B per lane, lane-linear) in an LDS slot; after
+// one barrier every wave reads all NWV blocks' fragments with ds_read_b128 (the same registers the
+// computing wave held) and runs z for its own columns, its W2 fragments loaded straight from the
+// packed image into registers one hidden block ahead (no wave of the workgroup shares them).
+// The hidden layer is computed 2C / (32 NWV CB) times per edge instead of 2C / (32 CB) times, its
+// ReLU/split VALU work is spread over the waves, and the grid has E/32 x 2C/(32 NWV CB) workgroups.
+// The next round's X runs after the current round's z (its W1 loads issued before), so with two
+// waves per SIMD one wave's VALU split runs beside the other's MFMAs.
+// ------------------------------------------------------------------------------------------------
+template <int CB, int NWV>
+__device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
+  extern __shared__ u4 lds_all[];
+  const int HB = a.C / 32;
+  const int ncb = 2 * a.C / 32;                 // 32-column blocks of z
+  constexpr int CPG = NWV * CB;                  // column blocks per workgroup
+  const int eblocks = (a.E + 31) / 32;
+  // workgroup -> (column group, edge block); consecutive ids share a column group (its W2 slab) and,
+  // after the remap, an XCD and its L2
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int eb = id % eblocks, cg = id / eblocks;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int e0 = eb * 32;
+  const u4* img = a.packed;
+
+  // pose fragment (B operand of X = W1' pose'^T): lane's edge, k = 8 hh + j; k = 9 is the 1.0 of b1
+  bf8 pp[3];
+  {
+    const int e = min(e0 + r, a.E - 1);
+    const float* pr = a.pose + (int64_t)e * kNin;
+    float v[8];
+    if (hh == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = pr[j];
+    } else {
+      v[0] = pr[8];
+      v[1] = 1.f;
+#pragma unroll
+      for (int j = 2; j < 8; ++j) v[j] = 0.f;
+    }
+    split8(v, pp);
+  }
+  // this wave's column blocks (past the last: clamped for loads, never stored)
+  int cbw[CB];
+  const u4* w2p[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    cbw[c] = cg * CPG + w * CB + c;
+    w2p[c] = img + w1_units(a.C) + (int64_t)min(cbw[c], ncb - 1) * HB * 6 * 64 + lane;
+  }
+  typedef u4 W2F[CB][6];
+  auto load_w2 = [&](int hb, W2F& f) {
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) f[c][k] = w2p[c][(int64_t)(hb * 6 + k) * 64];
+  };
+  // X of hidden block hb, ReLU'd and split, into LDS slot (buf, w)
+  u4 w1f[3];
+  auto load_w1 = [&](int hb) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) w1f[p] = img[(int64_t)(min(hb, HB - 1) * 3 + p) * 64 + lane];
+  };
+  auto x_store = [&](int buf, int hbx) {
+    bf8 wa[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) wa[p] = as_bf8(w1f[p]);
+    f16v X;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) X[i] = 0.f;
+    X = mma6(wa, pp, X);
+    // training: the first column group writes h^T (register i of lane (r, hh) is unit (i & 3) + 8 (i >> 2)
+    // + 4 hh of the block, edge e0 + r: each register's 32 lanes store 128 contiguous bytes of a row)
+    if (a.hT != nullptr && cg == 0 && hbx < HB && e0 + r < a.E) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        a.hT[(int64_t)(hbx * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh) * a.hts + e0 + r] = relu(X[i]);
+    }
+    u4* slot = lds_all + (buf * NWV + w) * 6 * 64 + lane;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float hv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hv[j] = relu(X[8 * s2 + j]);
+      bf8 hp[3];
+      split8(hv, hp);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) slot[(s2 * 3 + p) * 64] = as_u4(hp[p]);
+    }
+  };
+  f16v Z[CB], ZL[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Z[c][i] = ZL[c][i] = 0.f;
+  auto z_block = [&](int buf, int j, const W2F& f) {
+    const u4* slot = lds_all + (buf * NWV + j) * 6 * 64 + lane;
+    bf8 hp[2][3];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) hp[s2][p] = as_bf8(slot[(s2 * 3 + p) * 64]);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int c = 0; c < CB; ++c) {
+        bf8 wb[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) wb[p] = as_bf8(f[c][3 * s2 + p]);
+        mma6_2(hp[s2], wb, Z[c], ZL[c]);
+      }
+  };
+
+  const int rounds = (HB + NWV - 1) / NWV;
+  // W2 fragments of hidden blocks hb in set hb % 4, requested three blocks ahead (one block's z is 12 CB
+  // MFMAs per wave: too short to cover an L2 round trip under load); NWV % 4 == 0, so a round's
+  // blocks take the sets in a fixed order
+  static_assert(NWV % 4 == 0, "four W2 sets per round");
+  W2F f0, f1, f2, f3;
+  load_w1(w);
+  load_w2(0, f0);
+  if (1 < HB) load_w2(1, f1);
+  if (2 < HB) load_w2(2, f2);
+  x_store(0, w);
+  __syncthreads();
+#pragma unroll 1
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int buf = rd & 1;
+    const bool more = rd + 1 < rounds;
+    if (more) load_w1((rd + 1) * NWV + w);  // the next round's X, under this round's MFMAs
+#pragma unroll
+    for (int j = 0; j < NWV; j += 4) {
+      const int hb = rd * NWV + j;
+      if (hb + 3 < HB) load_w2(hb + 3, f3);
+      if (hb < HB) z_block(buf, j, f0);
+      if (hb + 4 < HB) load_w2(hb + 4, f0);
+      if (hb + 1 < HB) z_block(buf, j + 1, f1);
+      if (hb + 5 < HB) load_w2(hb + 5, f1);
+      if (hb + 2 < HB) z_block(buf, j + 2, f2);
+      if (hb + 6 < HB) load_w2(hb + 6, f2);
+      if (hb + 3 < HB) z_block(buf, j + 3, f3);
+    }
+    if (more) x_store(buf ^ 1, (rd + 1) * NWV + w);  // slot buf ^ 1: last read in round rd - 1, before the last barrier
+    __syncthreads();
+  }
+  // epilogue: accumulator register i of lane (r, hh) is edge e0 + (i & 3) + 8 (i >> 2) + 4 hh, column r
+  const int N = 2 * a.C;
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    if (cbw[c] >= ncb) continue;
+    const int col = cbw[c] * 32 + r;
+    const float bias = a.b2 != nullptr ? a.b2[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = e0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      if (e < a.E) a.z[(int64_t)e * N + col] = __fadd_rn(__fadd_rn(Z[c][i], ZL[c][i]), bias);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) encoder2_cb1_w4(FwdArgs a) { encoder2_body<1, 4>(a); }
+__global__ void __launch_bounds__(256) encoder2_cb2_w4(FwdArgs a) { encoder2_body<2, 4>(a); }
+__global__ void __launch_bounds__(512) encoder2_cb1_w8(FwdArgs a) { encoder2_body<1, 8>(a); }
+__global__ void __launch_bounds__(512) encoder2_cb2_w8(FwdArgs a) { encoder2_body<2, 8>(a); }
+
+template <int CB, int NWV>
+hipError_t launch2_cfg(void (*kern)(FwdArgs), const FwdArgs& a, hipStream_t st) {
+  const int64_t eblocks = (a.E + 31) / 32;
+  const int64_t groups = (2 * (int64_t)a.C / 32 + NWV * CB - 1) / (NWV * CB);
+  const int64_t grid = eblocks * groups;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  const size_t lds = (size_t)2 * NWV * 6 * 64 * 16;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NWV), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fwd2(int cb, int nwv, const FwdArgs& a, hipStream_t st) {
+  if (nwv == 8)
+    return cb == 2 ? launch2_cfg<2, 8>(encoder2_cb2_w8, a, st) : launch2_cfg<1, 8>(encoder2_cb1_w8, a, st);
+  return cb == 2 ? launch2_cfg<2, 4>(encoder2_cb2_w4, a, st) : launch2_cfg<1, 4>(encoder2_cb1_w4, a, st);
+}
+
 }  // namespace mrp_x6
 
 using namespace mrp_x6;
@@ -445,6 +636,8 @@ extern "C" int mrp_edge_encoder_fwd_split(const float* pose, const void* packed,
   a.packed = static_cast<const u4*>(packed);
   a.b2 = b2;
   a.z = z;
+  a.hT = nullptr;
+  a.hts = 0;
   a.E = num_edges;
   a.C = C;
   a.egroups = (num_edges + 127) / 128;
@@ -456,10 +649,44 @@ extern "C" int mrp_edge_encoder_fwd_split(const float* pose, const void* packed,
   // two column blocks unless that leaves fewer than 192 workgroups, the split from C = 1024 on (the
   // long hidden walks)
   const mrp_host::Tuning& tu = mrp_host::tuning();
+  // shared-hidden forms (encoder2_body) by default: (1 column block, 8 waves) when that gives at least
+  // 192 workgroups, else (1, 4).  Per shape (tools/enc_lab.cpp, us, per-wave hidden / (1, 4) / (1, 8)):
+  // E=1792 C=512 18.7 / 18.5 / 16.7, E=896 C=512 13.3 / 12.6 / 15.3, E=1792 C=1280 99.7 / 91.3 / 94.7,
+  // E=448 C=2048 55.4 / 60.5 / 52.6, E=512 C=1024 21.0 / 21.2 / 26.4; (2, x) slower everywhere
+  int v = tu.edge_split_v;
+  if (v < 0) v = ((int64_t)(num_edges + 31) / 32) * (2 * (int64_t)C / 256) >= 192 ? 3 : 1;
+  if (v >= 1) {  // 1 = (CB 1, 4 waves), 2 = (2, 4), 3 = (1, 8), 4 = (2, 8)
+    return launch_fwd2(v == 2 || v == 4 ? 2 : 1, v >= 3 ? 8 : 4, a, st);
+  }
   const int cb = tu.edge_split_cb ? tu.edge_split_cb : ((int64_t)a.egroups * (2 * C / 64) >= 192 ? 2 : 1);
   int ks = tu.edge_split_k ? tu.edge_split_k : (C >= 1024 ? 2 : 1);
   if ((C / 32) % 2 != 0) ks = 1;  // the split needs an even hidden block count
   const int64_t grid = (int64_t)a.egroups * (2 * (int64_t)C / (32 * cb));
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   return launch_fwd(cb, ks, a, grid, st);
+}
+
+extern "C" int mrp_edge_encoder_fwd_split_train(const float* pose, const void* packed, const float* b2,
+                                                int32_t num_edges, int32_t C, float* z, float* hT, int64_t hT_stride,
+                                                void* stream) {
+  if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
+  if (num_edges == 0 || C == 0) return hipSuccess;
+  if (C % 32 != 0 || !image_fits(C)) return hipErrorNotSupported;
+  if (!pose || !packed || !z || !hT || hT_stride < num_edges || (reinterpret_cast<uintptr_t>(packed) & 15))
+    return hipErrorInvalidValue;
+  FwdArgs a;
+  a.pose = pose;
+  a.packed = static_cast<const u4*>(packed);
+  a.b2 = b2;
+  a.z = z;
+  a.hT = hT;
+  a.hts = hT_stride;
+  a.E = num_edges;
+  a.C = C;
+  a.egroups = (num_edges + 127) / 128;
+  // the shared-hidden form whose first column group writes h^T (per-shape choice as the inference entry)
+  const mrp_host::Tuning& tu = mrp_host::tuning();
+  int v = tu.edge_split_v;
+  if (v < 1) v = ((int64_t)(num_edges + 31) / 32) * (2 * (int64_t)C / 256) >= 192 ? 3 : 1;
+  return launch_fwd2(v == 2 || v == 4 ? 2 : 1, v >= 3 ? 8 : 4, a, static_cast<hipStream_t>(stream));
 }

@@ -9,8 +9,10 @@ hipError_t launch_bwd_ntb(const AggArgs& a_in, const Geometry& g, hipStream_t st
   if constexpr (NT <= 8) {
     const AggArgs& a = a_in;
     const size_t lds = lds_bwd<NT>(g.cpb, COMPLETE && a.logits, g.lpc);
-    // exactly two slices per lane: both prefetched (film_bwd_fused PRE2)
-    if (g.vec == 4 && a.PV == 2 * g.lpc && tuning().bwd_pre2) {
+    // exactly two slices per lane: both prefetched (film_bwd_fused PRE2; bwd_pre2 = 2: not with a
+    // grad_x base, whose instantiation then prefetches the base rows instead)
+    const int pre2 = tuning().bwd_pre2;
+    if (g.vec == 4 && a.PV == 2 * g.lpc && (pre2 == 1 || (pre2 == 2 && !DXB))) {
       MRP_LAUNCH((mrp::film_bwd_fused<NT, NT, 4, COMPLETE, DXB, 1, true>), lds);
       return hipGetLastError();
     }

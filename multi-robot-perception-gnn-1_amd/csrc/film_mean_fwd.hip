@@ -72,7 +72,7 @@ Tuning& tuning() {
 
 extern "C" {
 
-int mrp_abi_version(void) { return 16; }
+int mrp_abi_version(void) { return 17; }
 
 int mrp_tuning_set(const char* name, int32_t value) {
   if (name == nullptr) return hipErrorInvalidValue;
@@ -97,7 +97,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"bwd_fused_lo", &t.bwd_fused_lo, 1, 256},
       {"bwd_fused_hi", &t.bwd_fused_hi, 1, 256},
       {"bwd_fused_cap", &t.bwd_fused_cap, 1, 64},
-      {"bwd_pre2", &t.bwd_pre2, 0, 1},
+      {"bwd_pre2", &t.bwd_pre2, 0, 2},
       {"bwd_regular_vec", &t.bwd_regular_vec, 1, 2},
       {"bwd_regular_lanes", &t.bwd_regular_lanes, 1, 64},
       {"bwd_regular_mfma", &t.bwd_regular_mfma, 0, 1},
@@ -109,6 +109,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"edge_fused", &t.edge_fused, 0, 4},
       {"edge_split_cb", &t.edge_split_cb, 0, 2},
       {"edge_split_k", &t.edge_split_k, 0, 2},
+      {"edge_split_v", &t.edge_split_v, -1, 4},
       {"gemm_split", &t.gemm_split, -1, 6},
   };
   for (const Knob& k : knobs) {

@@ -1062,11 +1062,26 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
         asm volatile("" : "+v"(tile));
         const float* W = Wt + tile;
         if (do_dx) {
+          // grad_x_base (a separate instantiation: it costs registers): all NT rows requested before the
+          // first is needed, so one memory round trip per slice is exposed instead of one per node — not
+          // with PRE2, whose second register set leaves no room for them (256 + 30 registers: one wave
+          // per SIMD), which loads each row where it adds it
+          constexpr bool kPreBase = DXB && !PRE2;
+          Frag<VEC> base[kPreBase ? NT : 1];
+          if constexpr (kPreBase) {
+#pragma unroll
+            for (int u = 0; u < NT; ++u) {
+              const int uu = u < n ? u : n - 1;
+              base[u] = load_frag<VEC, true>(at_bytes(dxbase + (int64_t)uu * a.dxbs, lane_off));
+            }
+          }
 #pragma unroll
           for (int u = 0; u < NT; ++u) {
             if (!COMPLETE && u >= n) break;
             Frag<VEC> acc;
-            if (DXB) {  // grad_x_base: a separate instantiation (it costs registers)
+            if constexpr (kPreBase) {
+              acc = base[u];
+            } else if constexpr (DXB) {
               acc = load_frag<VEC, true>(at_bytes(dxbase + (int64_t)u * a.dxbs, lane_off));
             } else {
 #pragma unroll
@@ -1576,8 +1591,10 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
   // a block's second channel may lie past C (odd C): its loads then read the first channel's rows
   auto hvalid = [&](int i, int h) { return blk_c(i) + h < a.C; };
 
-  mf4 gq[4], xn[4], gq2[4], xn2[4];
-  auto load_step = [&](int st, mf4 (&gr)[4], mf4 (&xr)[4]) {
+  // DXB: the grad_x base rows of a step travel with its G rows (prefetched a step ahead like them; loaded
+  // at the store they exposed a full memory round trip per step: 125 vs 77 us at configs[4])
+  mf4 gq[4], xn[4], gq2[4], xn2[4], bq[DXB ? 4 : 1], bq2[DXB ? 4 : 1];
+  auto load_step = [&](int st, mf4 (&gr)[4], mf4 (&xr)[4], mf4 (&br)[DXB ? 4 : 1]) {
     const int i = st / ngroups, g = st - i * ngroups;
     const int c = blk_c(i);
     const float* gbase = a.g + (int64_t)node0 * a.gs + (int64_t)c * a.P;
@@ -1586,6 +1603,16 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
     for (int bb = 0; bb < 4; ++bb) {
       const uint32_t off = goff4[bb] - (h1 ? 0u : (uint32_t)hq[bb] * (uint32_t)a.P * 4u);
       gr[bb] = __builtin_nontemporal_load(reinterpret_cast<const mf4*>(at_bytes(gbase, off + (uint32_t)g * 256u)));
+    }
+    if constexpr (DXB) {
+      if (a.want_dx) {
+        const float* dxbase = a.dxb + (int64_t)node0 * a.dxbs + (int64_t)c * a.P;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const uint32_t off = boff4[bb] - (h1 ? 0u : (uint32_t)hq[bb] * (uint32_t)a.P * 4u);
+          br[bb] = __builtin_nontemporal_load(reinterpret_cast<const mf4*>(at_bytes(dxbase, off + (uint32_t)g * 256u)));
+        }
+      }
     }
     if (a.want_dgb) {
       const float* xbase = a.x + (int64_t)node0 * a.xs + (int64_t)c * a.P;
@@ -1598,7 +1625,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
     }
   };
 
-  if (nsteps > 0) load_step(0, gq, xn);  // the first pixel group, ahead of the gamma loads
+  if (nsteps > 0) load_step(0, gq, xn, bq);  // the first pixel group, ahead of the gamma loads
   if (pitem) {
     float gm[NE];
 #pragma unroll
@@ -1639,7 +1666,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
   float wa[4];
   mf4 dacc = {0.f, 0.f, 0.f, 0.f};  // Gram: D[4q + r][jl] of the current block
   float sacc = 0.f;                 // S partial: row jl, this lane's pixels
-  auto compute_step = [&](int st, mf4 (&gr)[4], const mf4 (&xr)[4]) {
+  auto compute_step = [&](int st, mf4 (&gr)[4], const mf4 (&xr)[4], const mf4 (&br)[DXB ? 4 : 1]) {
     const int i = st / ngroups, g = st - i * ngroups;
     const int cbl = (w + 4 * i) * CB;  // first channel of the block within the workgroup
     const int c = c0 + cbl;
@@ -1661,7 +1688,6 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
       if (!rvalid[bb]) gr[bb] = mf4{0.f, 0.f, 0.f, 0.f};
     if (a.want_dx) {
       float* obase = a.out + (int64_t)node0 * a.os + (int64_t)c * a.P;
-      const float* dxbase = DXB ? a.dxb + (int64_t)node0 * a.dxbs + (int64_t)c * a.P : nullptr;
       mf4 acc[4];
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
@@ -1674,7 +1700,7 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
         mf4 o = {acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
         if (a.self_scale != 0.f) o += a.self_scale * gr[r];  // residual epilogue
         if (rvalid[r]) {
-          if (DXB) o += __builtin_nontemporal_load(reinterpret_cast<const mf4*>(at_bytes(dxbase, boff4[r] + (uint32_t)g * 256u)));
+          if constexpr (DXB) o += br[r];
           __builtin_nontemporal_store(o, reinterpret_cast<mf4*>(at_bytes(obase, ooff4[r] + (uint32_t)g * 256u)));
         }
       }
@@ -1720,11 +1746,11 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
   // software pipeline over the wave's (block, pixel group) steps: two register sets, the next step's
   // loads in flight under the current step's MFMAs (step 0 was issued in the prologue)
   for (int st = 0; st < nsteps; st += 2) {
-    if (st + 1 < nsteps) load_step(st + 1, gq2, xn2);
-    compute_step(st, gq, xn);
+    if (st + 1 < nsteps) load_step(st + 1, gq2, xn2, bq2);
+    compute_step(st, gq, xn, bq);
     if (st + 1 < nsteps) {
-      if (st + 2 < nsteps) load_step(st + 2, gq, xn);
-      compute_step(st + 1, gq2, xn2);
+      if (st + 2 < nsteps) load_step(st + 2, gq, xn, bq);
+      compute_step(st + 1, gq2, xn2, bq2);
     }
   }
   if (!a.want_dgb) return;

@@ -17,7 +17,10 @@ struct Tuning {
   // (tools/sweep_geometry.py smallbwd; 32 channels: 67.2 vs 60.8 us at C=1280 in round 1); 32x32
   // planes are unaffected (2 channels of 128 lanes)
   int bwd_fused_lo = 8, bwd_fused_hi = 128, bwd_fused_cap = 16;
-  int bwd_pre2 = 1;  // film_bwd_fused: prefetch both slices when a lane owns exactly two
+  // film_bwd_fused: prefetch both slices when a lane owns exactly two — unless a grad_x base is given
+  // (2): the base rows are then prefetched instead (configs[1] 217.7 -> 189.9 us with the base,
+  // tools/exp_bwd_dxb.py); 1: always, 0: never
+  int bwd_pre2 = 2;
   int bwd_regular_vec = 2, bwd_regular_lanes = 16;              // film_bwd_regular (N > 8, k-NN)
   // film_bwd_mfma (Gram and grad_x on the matrix cores; P % 64 == 0, 16-byte aligned operands) for
   // graphs of 9..16 nodes: regular (k-NN; 0 = film_bwd_regular) and complete (0 = film_bwd_dx + the
@@ -36,6 +39,9 @@ struct Tuning {
   int gemm_split = -1;  // split-bf16 compress GEMM: -1 per shape, 2 (128-row workgroups) or 4 (256-row)
   int edge_split_cb = 0;  // mrp_edge_encoder_fwd_split: 32-column blocks per wave (1 or 2; 0 per shape)
   int edge_split_k = 0;   // mrp_edge_encoder_fwd_split: hidden blocks over 1 or 2 wave sets (0 per shape)
+  // mrp_edge_encoder_fwd_split kernel: -1 per shape, 0 the per-wave hidden layer, 1..4 shared-hidden
+  // forms (CB, waves) = (1, 4), (2, 4), (1, 8), (2, 8)
+  int edge_split_v = -1;
   int edge_gemm = 1;  // edge encoder's second Linear: 64 x 64 tiles of 32 x 32 waves on 16x16x4 (0) or 32x32x2 (1) MFMAs
 };
 Tuning& tuning();

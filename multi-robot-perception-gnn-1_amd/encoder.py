@@ -76,6 +76,7 @@ _packed = weakref.WeakKeyDictionary()
 
 def clear_packed_weights() -> None:
     _packed.clear()
+    _w2t_cache.clear()
 
 
 def packed_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> torch.Tensor:
@@ -251,8 +252,108 @@ class EdgeEncoderFunction(torch.autograd.Function):
 
 
 #: calls per encoder path ("split": mrp_edge_encoder_fwd_split, "fused": mrp_edge_encoder_fwd,
-#: "autograd": EdgeEncoderFunction) — lets tests assert which kernels a forward actually ran
+#: "split_train": EdgeEncoderSplitFunction, "autograd": EdgeEncoderFunction) — lets tests assert which
+#: kernels a forward actually ran
 PATH_COUNTS = collections.Counter()
+
+
+_w2t_cache = weakref.WeakKeyDictionary()
+
+
+def transposed_w2(l2: torch.nn.Linear) -> torch.Tensor:
+    """W2^T (C, 2C) row-major — the dh^T GEMM's row operand — cached per weight version like the
+    packed images (cleared by :func:`clear_packed_weights`)."""
+    w2 = l2.weight
+    key = (w2.data_ptr(), w2._version, w2.device.index)
+    hit = _w2t_cache.get(l2)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    t = w2.detach().float().t().contiguous()
+    _w2t_cache[l2] = (key, t)
+    return t
+
+
+def split_train_supported(E: int, C: int) -> bool:
+    """The split-bf16 training path's shapes: C % 32 == 0 and E % 32 == 0 (its backward GEMMs walk
+    the edges in 32-edge stages); the reference configurations all qualify (E = B N (N - 1) or B N k)."""
+    return E > 0 and C > 0 and C % 32 == 0 and E % 32 == 0
+
+
+class EdgeEncoderSplitFunction(torch.autograd.Function):
+    """z = relu(pose W1^T + b1) W2^T + b2 (``models.py:146-149`` without the Sigmoid) on the split-bf16
+    matrix cores, forward and backward (``include/mrp_gnn.h``, the encoder's training path):
+
+    * forward: ``mrp_edge_encoder_fwd_split_train`` — the inference kernel, which also writes h^T;
+    * backward: on a side stream ``mrp_edge_encoder_bwd_prep`` (dz^T) and ``mrp_edge_encoder_bwd_split``
+      for dW2 = dz^T h (db2 = the row sums of dz^T on the same pass); beside it ``_bwd_split`` for
+      dh^T = W2^T dz^T and ``mrp_edge_encoder_bwd_t`` (the ReLU mask, dW1, db1).  Gradients are written straight into a
+      gradient all-reducer's buckets when one holds the parameters (``dist.grad_out_like``)."""
+
+    @staticmethod
+    def forward(ctx, pose, w1, b1, w2, b2, img, w2t):
+        E, C = pose.shape[0], w1.shape[0]
+        pose = pose.detach().contiguous().float()
+        b2c = b2.detach().contiguous().float() if b2 is not None else None
+        z = torch.empty((E, 2 * C), device=pose.device, dtype=torch.float32)
+        hT = torch.empty((C, E), device=pose.device, dtype=torch.float32)
+        lib = _lib.load_library()
+        with torch.cuda.device(pose.device):
+            _lib.check(lib.mrp_edge_encoder_fwd_split_train(
+                _ptr(pose), _ptr(img), _ptr(b2c) if b2c is not None else None, E, C, _ptr(z), _ptr(hT), E,
+                ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
+        ctx.save_for_backward(pose, w1, b1, w2, b2, hT, w2t)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        pose, w1, b1, w2, b2, hT, w2t = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        dz = dz.contiguous().float()
+        E, C = pose.shape[0], w1.shape[0]
+        dev = dz.device
+        cur = torch.cuda.current_stream(dev)
+        lib = _lib.load_library()
+        nbytes = int(lib.mrp_edge_encoder_bwd_split_workspace(E, C))
+
+        def workspace():
+            return torch.empty((nbytes + 3) // 4, device=dev) if nbytes > 0 else None
+
+        dw2 = db2 = side = None
+        with torch.cuda.device(dev):
+            if need[3] or need[4]:  # dz^T, then dW2 = dz^T h with db2 as its row sums, on the side stream
+                dw2 = _grad_out(w2, (2 * C, C), dev) if need[3] else torch.empty((2 * C, C), device=dev)
+                db2 = _grad_out(b2, (2 * C,), dev) if need[4] else None
+                dzT = torch.empty((2 * C, E), device=dev)
+                wsa = workspace()
+                side = _side_stream(dev)
+                side.wait_stream(cur)
+                ss = ctypes.c_void_p(side.cuda_stream)
+                _lib.check(lib.mrp_edge_encoder_bwd_prep(_ptr(dz), E, C, _ptr(dzT), E, ss), "mrp_edge_encoder_bwd_prep")
+                _lib.check(lib.mrp_edge_encoder_bwd_split(
+                    None, _ptr(dzT), None, _ptr(hT), E, C, None, _ptr(dw2), _ptr(db2) if db2 is not None else None,
+                    _ptr(wsa) if wsa is not None else None, nbytes, ss), "mrp_edge_encoder_bwd_split")
+                for t in (dz, hT, dzT, wsa, dw2, db2):
+                    if t is not None:
+                        t.record_stream(side)
+            dw1 = db1 = dhT = None
+            if need[0] or need[1] or need[2]:  # dh^T = W2^T dz^T, then the ReLU mask, dW1, db1
+                st = ctypes.c_void_p(cur.cuda_stream)
+                dhT = torch.empty((C, E), device=dev)
+                wsb = workspace()
+                _lib.check(lib.mrp_edge_encoder_bwd_split(
+                    _ptr(dz), None, _ptr(w2t), None, E, C, _ptr(dhT), None, None,
+                    _ptr(wsb) if wsb is not None else None, nbytes, st), "mrp_edge_encoder_bwd_split")
+                if need[1] or need[2]:
+                    dw1 = _grad_out(w1, (C, 9), dev) if need[1] else None
+                    db1 = _grad_out(b1, (C,), dev) if need[2] else None
+                    wst = torch.empty(max(int(lib.mrp_edge_encoder_bwd_t_workspace(E, C)) // 4, 1), device=dev)
+                    _lib.check(lib.mrp_edge_encoder_bwd_t(
+                        _ptr(dhT), E, _ptr(hT), E, _ptr(pose), E, C, _ptr(dw1) if dw1 is not None else None,
+                        _ptr(db1) if db1 is not None else None, _ptr(wst), wst.numel() * 4, st), "mrp_edge_encoder_bwd_t")
+            if side is not None:
+                cur.wait_stream(side)
+        dpose = (dhT * (hT > 0)).t().mm(w1.float()) if need[0] else None
+        return dpose, dw1, db1, dw2 if need[3] else None, db2, None, None
 
 
 def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Tensor:
@@ -273,5 +374,11 @@ def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Te
         if z is not None:
             PATH_COUNTS["fused"] += 1
             return z
+    C = l1.weight.shape[0]
+    if _LOGITS_PATH == "split" and split_train_supported(pose.shape[0], C) and l1.bias is not None \
+            and tuple(l1.weight.shape) == (C, 9) and tuple(l2.weight.shape) == (2 * C, C):
+        PATH_COUNTS["split_train"] += 1
+        return EdgeEncoderSplitFunction.apply(pose, l1.weight, l1.bias, l2.weight, l2.bias,
+                                              packed_weights(l1, l2), transposed_w2(l2))
     PATH_COUNTS["autograd"] += 1
     return EdgeEncoderFunction.apply(*params)

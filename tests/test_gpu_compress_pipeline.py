@@ -1,0 +1,76 @@
+"""The split-bf16 compress forward / data-gradient kernel forms (``csrc/compress_split.hip``; knob
+``gemm_split``): 2 = 128-row workgroups, 4 = 256-row with 32-k stages, 5 = the pipelined 256-row form
+(16-k stages in a ring of four LDS buffers, both operands by LDS-DMA with counted waits, the default
+where M % 256 == 0), 6 = two pipelined 128-row workgroups per CU.  All of them accumulate the same
+partial products in the same k order, so their outputs must be bit-identical — across ragged M and
+column tails, the shortest K (two 16-k stages), planes smaller than a column tile — and every launch
+of one kernel must repeat the last bit for bit at a BASELINE config size (the guard against an
+LDS-DMA ordering race: a read that overtakes the DMA it depends on gives rare, shifting errors).
+Accuracy against float64 is tests/test_gpu_compress_gemm.py's."""
+import contextlib
+
+import pytest
+import torch
+
+import mrp_gnn_amd as m
+
+pytestmark = pytest.mark.gpu
+
+FORMS = (2, 4, 5, 6)
+
+
+@contextlib.contextmanager
+def _form(v):
+    lib = m.load_library()
+    prev = m.compress.compress_path()
+    m.compress.set_compress_path("split")
+    assert lib.mrp_tuning_set(b"gemm_split", v) == 0
+    try:
+        yield
+    finally:
+        lib.mrp_tuning_set(b"gemm_split", -1)
+        m.compress.set_compress_path(prev)
+
+
+@pytest.mark.parametrize("n,C,H,W", [(3, 32, 2, 2), (5, 64, 4, 4), (7, 160, 4, 8), (2, 256, 8, 8), (9, 288, 2, 6),
+                                     (33, 96, 8, 8), (4, 512, 16, 16), (1, 256, 1, 4), (17, 320, 4, 4)])
+def test_forms_bit_identical(cuda_device, n, C, H, W):
+    torch.manual_seed(n * 7 + C)
+    dev = cuda_device
+    w = torch.randn(C, 2 * C, 1, 1, device=dev) / (2 * C) ** 0.5
+    b = torch.randn(C, device=dev)
+    x, a, gy = (torch.randn(n, C, H, W, device=dev) for _ in range(3))
+    outs = []
+    for v in FORMS:
+        with _form(v):
+            y = m.compress.compress_forward(w, b, x, a)
+            gx, ga = m.compress.compress_backward_data(w, gy)
+        torch.cuda.synchronize()
+        outs.append((v, y, gx, ga))
+    v0, y0, gx0, ga0 = outs[0]
+    for v, y, gx, ga in outs[1:]:
+        assert torch.equal(y, y0), (v, float((y - y0).abs().max()))
+        assert torch.equal(gx, gx0), (v, float((gx - gx0).abs().max()))
+        assert torch.equal(ga, ga0), (v, float((ga - ga0).abs().max()))
+
+
+@pytest.mark.parametrize("form", [5, 6])
+def test_config1_size_repeats_bit_identical(cuda_device, form):
+    """configs[1]'s layer shape (128 nodes, C = 512, 32 x 32): forward, data gradient and weight
+    gradient launched repeatedly on the same inputs give the same bits every time."""
+    torch.manual_seed(11)
+    dev = cuda_device
+    n, C, H, W = 128, 512, 32, 32
+    w = torch.randn(C, 2 * C, 1, 1, device=dev) / (2 * C) ** 0.5
+    b = torch.randn(C, device=dev)
+    x, a, gy = (torch.randn(n, C, H, W, device=dev) for _ in range(3))
+    with _form(form):
+        y0 = m.compress.compress_forward(w, b, x, a)
+        d0 = m.compress.compress_backward_data(w, gy)
+        w0 = m.compress.compress_backward_weight(gy, x, a)
+        for _ in range(4):
+            assert torch.equal(m.compress.compress_forward(w, b, x, a), y0)
+            d = m.compress.compress_backward_data(w, gy)
+            assert torch.equal(d[0], d0[0]) and torch.equal(d[1], d0[1])
+            g = m.compress.compress_backward_weight(gy, x, a)
+            assert torch.equal(g[0], w0[0]) and torch.equal(g[1], w0[1])

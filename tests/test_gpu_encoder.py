@@ -177,19 +177,24 @@ def test_edge_logits_takes_fused_kernel_only_without_grad(cuda_device):
 
 @pytest.mark.parametrize("E,C", [(1, 32), (31, 32), (33, 64), (127, 96), (129, 128), (1792, 512), (448, 2048),
                                  (300, 1024)])
-@pytest.mark.parametrize("cb,ks", [(1, 1), (2, 1), (1, 2), (2, 2)])
-def test_split_encoder_vs_float64(cuda_device, E, C, cb, ks):
-    """mrp_edge_encoder_fwd_split (three-way bf16 split, six partial products; one or two 32-column
-    blocks per wave; the hidden blocks walked by one wave set or split over two, C % 64 == 0) is as
-    accurate as an fp32 evaluation of the reference layers (float64 yardstick), for ragged edge
-    counts (partial 32-edge waves and 128-edge workgroups), C from one hidden block (no split
-    possible: one set) to 64, poses of robot-scale magnitudes."""
+@pytest.mark.parametrize("v,cb,ks", [(0, 1, 1), (0, 2, 1), (0, 1, 2), (0, 2, 2), (1, 0, 0), (2, 0, 0), (3, 0, 0),
+                                     (4, 0, 0), (-1, 0, 0)])
+def test_split_encoder_vs_float64(cuda_device, E, C, v, cb, ks):
+    """mrp_edge_encoder_fwd_split (three-way bf16 split, six partial products) in every form — the
+    per-wave hidden layer (v 0: one or two 32-column blocks per wave; the hidden blocks walked by one
+    wave set or split over two, C % 64 == 0) and the shared-hidden forms (v 1..4: the hidden layer
+    computed once per workgroup of 4 or 8 waves, 1 or 2 column blocks per wave; -1: the per-shape
+    default) — is as accurate as an fp32 evaluation of the reference layers (float64 yardstick), for
+    ragged edge counts (partial 32-edge blocks and workgroups), C from one hidden block to 64,
+    column groups past 2C, poses of robot-scale magnitudes."""
     torch.manual_seed(E * 3 + C)
     enc = m.edge_encoder([C, C]).to(cuda_device)
     pose = (torch.randn(E, 9) * 8).to(cuda_device)
     lib = m.load_library()
-    assert lib.mrp_tuning_set(b"edge_split_cb", cb) == 0
-    assert lib.mrp_tuning_set(b"edge_split_k", ks) == 0
+    assert lib.mrp_tuning_set(b"edge_split_v", v) == 0
+    if v == 0:
+        assert lib.mrp_tuning_set(b"edge_split_cb", cb) == 0
+        assert lib.mrp_tuning_set(b"edge_split_k", ks) == 0
     try:
         with torch.no_grad():
             z = m.encoder.encoder_forward_split(pose, enc.layers[0], enc.layers[2])

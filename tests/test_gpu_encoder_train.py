@@ -1,0 +1,70 @@
+"""The edge encoder's training path on the split-bf16 matrix cores (encoder.EdgeEncoderSplitFunction:
+mrp_edge_encoder_fwd_split_train, _bwd_prep, _bwd_split, _bwd_t) — the reference's Linear / ReLU /
+Linear (``dgl/model/models.py:146-149``) under ``loss.backward()`` (``dgl/training.py:208-210``).
+Every parameter gradient, the logits and the pose gradient are judged against a float64 evaluation
+of the reference layers with the fp32 yardstick (``stack_ref.within``), at the BASELINE shapes
+(E, C) = (1792, 512), (448, 2048), (512, 1024) and small ones; the path taken is asserted."""
+import pytest
+import torch
+
+import mrp_gnn_amd as m
+import stack_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _reference(enc, pose, gz, dtype):
+    ps = [p.detach().to(dtype).requires_grad_(True) for p in enc.parameters()]
+    pz = pose.detach().to(dtype).requires_grad_(True)
+    z = torch.nn.functional.linear(torch.relu(torch.nn.functional.linear(pz, ps[0], ps[1])), ps[2], ps[3])
+    z.backward(gz.to(dtype))
+    return z.detach(), [p.grad for p in ps], pz.grad
+
+
+@pytest.mark.parametrize("E,C", [(1792, 512), (448, 2048), (512, 1024), (96, 64), (32, 32), (224, 160)])
+def test_split_training_encoder_vs_float64(cuda_device, E, C):
+    torch.manual_seed(E + 7 * C)
+    enc = m.edge_encoder([C, C]).to(cuda_device)
+    pose = (torch.randn(E, 9) * 8).to(cuda_device).requires_grad_(True)
+    gz = torch.randn(E, 2 * C, device=cuda_device)
+    before = m.encoder.PATH_COUNTS["split_train"]
+    z = m.encoder.edge_logits(enc.layers, pose)
+    assert m.encoder.PATH_COUNTS["split_train"] == before + 1
+    z.backward(gz)
+    z32, g32, p32 = _reference(enc, pose, gz, torch.float32)
+    z64, g64, p64 = _reference(enc, pose, gz, torch.float64)
+    ok, errs = stack_ref.within(z.detach(), z32, z64)
+    assert ok, ("z", errs)
+    for name, p, a32, a64 in zip(("w1", "b1", "w2", "b2"), enc.parameters(), g32, g64):
+        ok, errs = stack_ref.within(p.grad, a32, a64)
+        assert ok, (name, errs)
+    ok, errs = stack_ref.within(pose.grad, p32, p64)
+    assert ok, ("pose", errs)
+
+
+def test_split_training_encoder_deterministic_and_repacks(cuda_device):
+    """Two backward passes give bit-identical gradients (fixed-order sums, no atomics); after an
+    optimizer-style in-place update the packed image and W2^T follow the new weights."""
+    torch.manual_seed(3)
+    E, C = 448, 256
+    enc = m.edge_encoder([C, C]).to(cuda_device)
+    pose = (torch.randn(E, 9) * 8).to(cuda_device)
+    gz = torch.randn(E, 2 * C, device=cuda_device)
+    grads = []
+    for _ in range(2):
+        enc.zero_grad(set_to_none=True)
+        m.encoder.edge_logits(enc.layers, pose).backward(gz)
+        grads.append([p.grad.clone() for p in enc.parameters()])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+    with torch.no_grad():
+        for p in enc.parameters():
+            p.mul_(-0.5)
+    enc.zero_grad(set_to_none=True)
+    z = m.encoder.edge_logits(enc.layers, pose)
+    z.backward(gz)
+    z32, g32, _ = _reference(enc, pose, gz, torch.float32)
+    z64, g64, _ = _reference(enc, pose, gz, torch.float64)
+    assert stack_ref.within(z.detach(), z32, z64)[0]
+    for p, a32, a64 in zip(enc.parameters(), g32, g64):
+        assert stack_ref.within(p.grad, a32, a64)[0]

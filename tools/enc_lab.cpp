@@ -1,0 +1,135 @@
+// Kernel lab (not product code): mrp_edge_encoder_fwd_split variants (mrp_tuning_set "edge_split_v",
+// 0 = per-wave hidden layer, 1..4 = shared-hidden forms) at the BASELINE encoder shapes, checked on
+// sampled outputs against a float64 host evaluation and element-wise against variant 0, timed with
+// hipEvents (median of rounds, variants interleaved).
+// build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/enc_lab.cpp -I include \
+//        -L multi-robot-perception-gnn-1_amd/lib -lmrp_gnn -Wl,-rpath,'$ORIGIN/../../multi-robot-perception-gnn-1_amd/lib' -o tools/bin/enc_lab
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "mrp_gnn.h"
+
+#define CK(x)                                                                                    \
+  do {                                                                                           \
+    auto e_ = (x);                                                                               \
+    if (e_ != 0) {                                                                               \
+      fprintf(stderr, "%s:%d %s -> %d\n", __FILE__, __LINE__, #x, (int)e_);                      \
+      exit(2);                                                                                   \
+    }                                                                                            \
+  } while (0)
+
+int main(int argc, char** argv) {
+  std::string vs = argc > 1 ? argv[1] : "0,1,2,3,4";
+  int iters = argc > 2 ? atoi(argv[2]) : 20;
+  std::vector<int> variants;
+  for (size_t i = 0; i < vs.size();) {
+    size_t j = vs.find(',', i);
+    if (j == std::string::npos) j = vs.size();
+    variants.push_back(atoi(vs.substr(i, j - i).c_str()));
+    i = j + 1;
+  }
+  struct Sh {
+    int E, C;
+  } shapes[] = {{1792, 512}, {896, 512}, {1792, 1280}, {448, 2048}, {512, 1024}, {100, 64}, {31, 32}};
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  bool all_ok = true;
+  for (auto sh : shapes) {
+    const int E = sh.E, C = sh.C;
+    std::mt19937 rng(E + C);
+    std::normal_distribution<float> nd(0.f, 1.f);
+    std::vector<float> pose(E * 9), w1(C * 9), b1(C), w2((size_t)2 * C * C), b2(2 * C);
+    for (auto& v : pose) v = nd(rng) * 8;
+    for (auto& v : w1) v = nd(rng) / 3;
+    for (auto& v : b1) v = nd(rng) / 3;
+    for (auto& v : w2) v = nd(rng) / std::sqrt((float)C);
+    for (auto& v : b2) v = nd(rng) / std::sqrt((float)C);
+    float *dp, *dw1, *db1, *dw2, *db2, *dz;
+    void* img;
+    CK(hipMalloc(&dp, pose.size() * 4));
+    CK(hipMalloc(&dw1, w1.size() * 4));
+    CK(hipMalloc(&db1, b1.size() * 4));
+    CK(hipMalloc(&dw2, w2.size() * 4));
+    CK(hipMalloc(&db2, b2.size() * 4));
+    CK(hipMalloc(&dz, (size_t)E * 2 * C * 4));
+    CK(hipMalloc(&img, mrp_edge_encoder_pack_bytes(C)));
+    CK(hipMemcpy(dp, pose.data(), pose.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw1, w1.data(), w1.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db1, b1.data(), b1.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw2, w2.data(), w2.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db2, b2.data(), b2.size() * 4, hipMemcpyHostToDevice));
+    CK(mrp_edge_encoder_pack(dw1, db1, dw2, C, img, st));
+    // float64 reference of sampled rows
+    std::vector<int> rows;
+    for (int i = 0; i < 24; ++i) rows.push_back((int)(rng() % E));
+    rows.push_back(E - 1);
+    std::vector<std::vector<double>> ref;
+    double maxref = 0;
+    for (int e : rows) {
+      std::vector<double> h(C), z(2 * C);
+      for (int u = 0; u < C; ++u) {
+        double a = b1[u];
+        for (int k = 0; k < 9; ++k) a += (double)w1[u * 9 + k] * pose[e * 9 + k];
+        h[u] = a > 0 ? a : 0;
+      }
+      for (int j = 0; j < 2 * C; ++j) {
+        double a = b2[j];
+        for (int u = 0; u < C; ++u) a += (double)w2[(size_t)j * C + u] * h[u];
+        z[j] = a;
+        maxref = std::max(maxref, std::fabs(a));
+      }
+      ref.push_back(z);
+    }
+    std::vector<std::vector<float>> outs;
+    std::vector<std::vector<double>> times(variants.size());
+    for (size_t vi = 0; vi < variants.size(); ++vi) {
+      CK(mrp_tuning_set("edge_split_v", variants[vi]));
+      CK(hipMemset(dz, 0xff, (size_t)E * 2 * C * 4));
+      CK(mrp_edge_encoder_fwd_split(dp, img, db2, E, C, dz, st));
+      CK(hipStreamSynchronize(st));
+      std::vector<float> h((size_t)E * 2 * C);
+      CK(hipMemcpy(h.data(), dz, h.size() * 4, hipMemcpyDeviceToHost));
+      outs.push_back(std::move(h));
+    }
+    for (int r = 0; r < 5; ++r)
+      for (size_t vi = 0; vi < variants.size(); ++vi) {
+        CK(mrp_tuning_set("edge_split_v", variants[vi]));
+        CK(mrp_edge_encoder_fwd_split(dp, img, db2, E, C, dz, st));
+        CK(hipEventRecord(e0, st));
+        for (int i = 0; i < iters; ++i) CK(mrp_edge_encoder_fwd_split(dp, img, db2, E, C, dz, st));
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        times[vi].push_back(ms * 1e3 / iters);
+      }
+    for (size_t vi = 0; vi < variants.size(); ++vi) {
+      double err = 0, d0 = 0;
+      for (size_t i = 0; i < rows.size(); ++i)
+        for (int j = 0; j < 2 * C; ++j)
+          err = std::max(err, std::fabs((double)outs[vi][(size_t)rows[i] * 2 * C + j] - ref[i][j]));
+      for (size_t i = 0; i < outs[0].size(); ++i) d0 = std::max(d0, (double)std::fabs(outs[vi][i] - outs[0][i]));
+      auto t = times[vi];
+      std::sort(t.begin(), t.end());
+      const bool ok = err / maxref < 2e-6 && std::isfinite(d0);
+      all_ok = all_ok && ok;
+      printf("E=%5d C=%5d v=%d  %7.2f us (min %7.2f)  f64 err %.2e  vs v0 %.2e %s\n", E, C, variants[vi], t[2], t[0],
+             err / maxref, d0 / maxref, ok ? "" : "FAIL");
+      fflush(stdout);
+    }
+    CK(mrp_tuning_set("edge_split_v", 0));
+    for (void* p : {(void*)dp, (void*)dw1, (void*)db1, (void*)dw2, (void*)db2, (void*)dz, img}) CK(hipFree(p));
+  }
+  printf(all_ok ? "ALL OK\n" : "SOME FAIL\n");
+  return all_ok ? 0 : 1;
+}
