@@ -422,7 +422,7 @@ hipError_t launch_fwd(int cb, int ks, const FwdArgs& a, int64_t grid, hipStream_
 // The next round's X runs after the current round's z (its W1 loads issued before), so with two
 // waves per SIMD one wave's VALU split runs beside the other's MFMAs.
 // ------------------------------------------------------------------------------------------------
-template <int CB, int NWV>
+template <int CB, int NWV, int ABL = 0>  // ABL: lab ablation bits (tools/enc_ablate.hip; 0 in the library)
 __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
   extern __shared__ u4 lds_all[];
   const int HB = a.C / 32;
@@ -471,7 +471,12 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
 #pragma unroll
     for (int c = 0; c < CB; ++c)
 #pragma unroll
-      for (int k = 0; k < 6; ++k) f[c][k] = w2p[c][(int64_t)(hb * 6 + k) * 64];
+      for (int k = 0; k < 6; ++k) {
+        if (ABL & 1)
+          f[c][k] = u4{(uint32_t)hb, (uint32_t)k, (uint32_t)lane, 0u};
+        else
+          f[c][k] = w2p[c][(int64_t)(hb * 6 + k) * 64];
+      }
   };
   // X of hidden block hb, ReLU'd and split, into LDS slot (buf, w)
   u4 w1f[3];
@@ -486,7 +491,7 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
     f16v X;
 #pragma unroll
     for (int i = 0; i < 16; ++i) X[i] = 0.f;
-    X = mma6(wa, pp, X);
+    if (!(ABL & 2)) X = mma6(wa, pp, X);
     // training: the first column group writes h^T (register i of lane (r, hh) is unit (i & 3) + 8 (i >> 2)
     // + 4 hh of the block, edge e0 + r: each register's 32 lanes store 128 contiguous bytes of a row)
     if (a.hT != nullptr && cg == 0 && hbx < HB && e0 + r < a.E) {
@@ -495,6 +500,7 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
         a.hT[(int64_t)(hbx * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh) * a.hts + e0 + r] = relu(X[i]);
     }
     u4* slot = lds_all + (buf * NWV + w) * 6 * 64 + lane;
+    if (ABL & 64) return;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       float hv[8];
@@ -517,7 +523,9 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) hp[s2][p] = as_bf8(slot[(s2 * 3 + p) * 64]);
+      for (int p = 0; p < 3; ++p)
+        hp[s2][p] = (ABL & 16) ? as_bf8(u4{(uint32_t)j, (uint32_t)p, (uint32_t)lane, (uint32_t)s2})
+                               : as_bf8(slot[(s2 * 3 + p) * 64]);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -525,7 +533,12 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
         bf8 wb[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) wb[p] = as_bf8(f[c][3 * s2 + p]);
-        mma6_2(hp[s2], wb, Z[c], ZL[c]);
+        if (ABL & 8) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) Z[c][p] += __builtin_bit_cast(float, as_u4(hp[s2][p]).x ^ as_u4(wb[p]).x);
+        } else {
+          mma6_2(hp[s2], wb, Z[c], ZL[c]);
+        }
       }
   };
 
@@ -559,7 +572,7 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
       if (hb + 3 < HB) z_block(buf, j + 3, f3);
     }
     if (more) x_store(buf ^ 1, (rd + 1) * NWV + w);  // slot buf ^ 1: last read in round rd - 1, before the last barrier
-    __syncthreads();
+    if (!(ABL & 4)) __syncthreads();
   }
   // epilogue: accumulator register i of lane (r, hh) is edge e0 + (i & 3) + 8 (i >> 2) + 4 hh, column r
   const int N = 2 * a.C;
@@ -571,7 +584,8 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int e = e0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-      if (e < a.E) a.z[(int64_t)e * N + col] = __fadd_rn(__fadd_rn(Z[c][i], ZL[c][i]), bias);
+      const float v = __fadd_rn(__fadd_rn(Z[c][i], ZL[c][i]), bias);
+      if ((ABL & 32) ? (v == 1.2345f && e < a.E) : e < a.E) a.z[(int64_t)e * N + col] = v;
     }
   }
 }
