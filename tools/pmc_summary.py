@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Summarise a ``tools/profile_r02.sh`` output directory into committed profiles/ files.
+"""Summarise a ``tools/profile_round.sh`` output directory into committed profiles/ files.
 
-    python tools/pmc_summary.py gpurun_out/prof_r02 r02
+    python tools/pmc_summary.py gpurun_out/prof_r04 r04
 
 Writes
   profiles/<round>_bench_kernel_stats.csv  rocprofv3 --stats of the headline bench command

@@ -1,10 +1,11 @@
 #!/bin/bash
 # Profile the aggregation kernels at every BASELINE config shape (tools/prof_kernels.py), a training
-# step of every config (tools/prof_train_step.py) and the headline bench command on the GPU box:
+# step of every config (tools/prof_train_step.py), the headline layer's training step
+# (tools/exp_headline_train.py) and the headline bench command on the GPU box:
 # kernel trace + stats, then one PMC pass per counter group (aggregation kernels; the matrix-core
 # compress GEMMs and the encoder)
 # (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950; <= 8 SQ counters per pass).
-# Usage: tools/profile_r03.sh <round> ; output under gpurun_out/prof_<round>/, summarised into
+# Usage: tools/profile_round.sh <round> ; output under gpurun_out/prof_<round>/, summarised into
 # profiles/ by tools/pmc_summary.py.
 set -euo pipefail
 R=${1:-r03}
@@ -20,7 +21,9 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/bench" -o run --outp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
   -- python3 tools/prof_kernels.py "$ITERS" > "$OUT/trace.log" 2>&1
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/train" -o run --output-format csv \
-  -- python3 tools/prof_train_step.py 5 > "$OUT/train.log" 2>&1
+  -- python3 tools/prof_train_step.py 5 1 2 3 4 --no-fwd > "$OUT/train.log" 2>&1
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/headline_train" -o run --output-format csv \
+  -- python3 tools/exp_headline_train.py 20 > "$OUT/headline_train.log" 2>&1
 pass() {  # name counters...
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" --kernel-include-regex "film_" -d "$OUT/pmc_$name" -o run \
@@ -37,5 +40,5 @@ for op in fwd dgrad wgrad; do
     --kernel-include-regex "gemm_n" -d "$OUT/pmc_gemm_$op" -o run --output-format csv -- python3 tools/prof_compress.py 5 $op > "$OUT/pmc_gemm_$op.log" 2>&1
 done
 timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES \
-  --kernel-include-regex "encoder_fwd" -d "$OUT/pmc_encoder" -o run --output-format csv -- python3 tools/prof_encoder.py 5 2 > "$OUT/pmc_encoder.log" 2>&1
+  --kernel-include-regex "encoder" -d "$OUT/pmc_encoder" -o run --output-format csv -- python3 tools/prof_encoder.py 5 > "$OUT/pmc_encoder.log" 2>&1
 echo "profile $R done"
