@@ -1,0 +1,120 @@
+"""Property-based tests (hypothesis) of the host-side graph logic and the CPU oracle — SURVEY §4
+item 2: arbitrary batches of graphs with up to 16 nodes (``MRP_MAX_NODES``), arbitrary in-degrees
+(zero, multi-edges, self-loops), channels and plane sizes.  The GPU kernels get the same strategies
+against the oracle in tests/test_gpu_properties.py."""
+import numpy as np
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+import importlib
+
+import mrp_gnn_amd as m
+import oracle
+from graph_strategies import batches
+
+G = importlib.import_module(m.__name__ + ".graph")  # the module (m.graph is the dgl.graph-like constructor)
+
+SETTINGS = settings(max_examples=60, deadline=None, derandomize=True, database=None,
+                    suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+
+
+@SETTINGS
+@given(batches())
+def test_csr_is_the_dgl_mailbox_order(case):
+    """build_csr: in-edges of every destination in increasing edge id (DGL's mailbox order, the
+    reference's reduction order), degrees = bincount, eid a permutation, src consistent."""
+    bnn, src, dst = case
+    N = int(sum(bnn))
+    indptr, csrc, eid, goff, max_nodes = G.build_csr(src, dst, N, bnn)
+    assert indptr[0] == 0 and indptr[-1] == len(src)
+    assert np.all(np.diff(indptr) == np.bincount(np.asarray(dst, np.int64), minlength=N))
+    assert sorted(eid.tolist()) == list(range(len(src)))
+    assert np.array_equal(csrc, np.asarray(src)[eid])
+    for v in range(N):
+        seg = eid[indptr[v]:indptr[v + 1]]
+        assert np.all(np.diff(seg) > 0)
+        assert np.all(np.asarray(dst)[seg] == v)
+    assert max_nodes == (max(bnn) if bnn else 0)
+    assert np.array_equal(goff, np.concatenate([[0], np.cumsum(bnn)]))
+
+
+@SETTINGS
+@given(batches())
+def test_batch_unbatch_round_trip(case):
+    bnn, src, dst = case
+    goff = np.concatenate([[0], np.cumsum(bnn)])
+    graphs = []
+    for i, n in enumerate(bnn):
+        sel = [k for k in range(len(src)) if goff[i] <= dst[k] < goff[i + 1]]
+        graphs.append(m.RobotGraph([src[k] - goff[i] for k in sel], [dst[k] - goff[i] for k in sel], num_nodes=n))
+    g = m.batch(graphs)
+    assert g.num_nodes() == sum(bnn)
+    back = m.unbatch(g)
+    assert len(back) == len(graphs)
+    for a, b in zip(back, graphs):
+        assert a.num_nodes() == b.num_nodes()
+        for x, y in zip(a.edges(), b.edges()):
+            assert torch.equal(x, y)
+
+
+@SETTINGS
+@given(st.integers(2, 16), st.data())
+def test_knn_edges_regular(n, data):
+    k = data.draw(st.integers(1, n - 1))
+    pos = np.asarray(data.draw(st.lists(st.tuples(*[st.floats(-50, 50, allow_nan=False)] * 3), min_size=n, max_size=n)))
+    src, dst = m.knn_edges(pos, k)
+    src, dst = np.asarray(src), np.asarray(dst)
+    assert np.all(np.bincount(dst, minlength=n) == k)
+    assert not np.any(src == dst)
+    for v in range(n):
+        s = src[dst == v]
+        assert np.all(np.diff(s) > 0)  # ascending sources, no duplicates
+
+
+@SETTINGS
+@given(st.integers(1, 16), st.integers(1, 4))
+def test_complete_batch_detection(n, B):
+    g = m.batch([m.complete_graph(n) for _ in range(B)])
+    s, d = (t.numpy() for t in g.edges())
+    assert G.is_complete_batch(s, d, [n] * B)
+    if len(s) >= 2:
+        s2 = s.copy()
+        s2[[0, 1]] = s2[[1, 0]]
+        assert not G.is_complete_batch(s2, d, [n] * B) or np.array_equal(s2, s)
+
+
+def _dense_reference(x, gb, src, dst, mode):
+    """The FiLM aggregate as dense float64 sums over each destination's in-edges (any order)."""
+    N = x.shape[0]
+    out = np.zeros(x.shape, np.float64)
+    deg = np.bincount(np.asarray(dst, np.int64), minlength=N)
+    xd, g = x.double().numpy(), gb.double().numpy()
+    for e, (u, v) in enumerate(zip(src, dst)):
+        if mode == "copy_mean":
+            out[v] += xd[u]
+        else:
+            out[v] += g[e, :, 0][:, None, None] * xd[u] + g[e, :, 1][:, None, None]
+    if mode in ("film_mean", "copy_mean"):
+        out /= np.maximum(deg, 1)[:, None, None, None]
+    return out
+
+
+@SETTINGS
+@given(batches(), st.integers(1, 12), st.integers(1, 5), st.integers(1, 5),
+       st.sampled_from(["film_mean", "film_sum", "copy_mean"]), st.integers(0, 2 ** 31 - 1))
+def test_oracle_matches_dense_sums(case, C, H, W, mode, seed):
+    """The oracle's DGL-bucketed UDF execution equals the order-free float64 definition to fp32
+    accuracy, for any topology (the oracle is the checker of every GPU test)."""
+    bnn, src, dst = case
+    N = int(sum(bnn))
+    gen = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, C, H, W, generator=gen)
+    gb = torch.rand(len(src), C, 2, generator=gen)
+    out = oracle.film_aggregate(x, gb, np.asarray(src, np.int64), np.asarray(dst, np.int64), mode).numpy()
+    ref = _dense_reference(x, gb, src, dst, mode)
+    assert out.shape == ref.shape
+    if ref.size == 0:
+        return
+    scale = max(np.abs(ref).max(), 1e-30)
+    assert np.abs(out - ref).max() / scale <= 1e-5
