@@ -4,9 +4,10 @@
 Headline workload (SURVEY.md §8(d) north-star target): per rank B=32 per-frame graphs of N=8 robots
 (complete directed graphs, the reference's ``dgl/dataloader.py:88-95``), node features
 C=512 x 32 x 32 fp32 (ResNet18 width at H/8 x W/8 of a 256^2 image), synthetic and seeded, already
-resident in HBM.  A *step* is one forward pass of the drop-in ``GCN`` layer over that batch: edge
-encoder (9 -> C -> 2C Linear/ReLU/Linear on the 1792 edge poses: HIP hidden-layer kernel + library
-GEMM) + the HIP FiLM-mean aggregation (which applies the encoder's sigmoid).  value = elements
+resident in HBM.  A *step* is one forward pass of the drop-in ``GCN`` layer over that batch, as the
+reference's eval loop runs it (no gradient): edge encoder (9 -> C -> 2C Linear/ReLU/Linear on the 1792
+edge poses in ONE HIP launch on the bf16 matrix cores at fp32 accuracy, ``mrp_edge_encoder_fwd_split``)
++ the HIP FiLM-mean aggregation (which applies the encoder's sigmoid).  value = elements
 (Nt*C*H*W) aggregated per second over all ranks.
 
 Multi-GPU (``torch.distributed.run``, one process per GPU): graphs of a batch are independent, so

@@ -1,23 +1,22 @@
 """Edge encoder on the GPU (``dgl/model/models.py:146-154``), restructured for the hot path.
 
-``z = W2 relu(W1 pose + b1) + b2``, ``gamma/beta = sigmoid(z)``:
+``z = W2 relu(W1 pose + b1) + b2``, ``gamma/beta = sigmoid(z)``; the sigmoid is not run here: the
+aggregation kernels take the logits (``MRP_AGG_GB_LOGITS``) and apply it while building their tiles.
 
-* ``relu(W1 pose + b1)`` — one HIP kernel (``mrp_edge_hidden_fwd``; K = 9, a streaming write);
-* ``h W2^T + b2``        — the encoder's only dense contraction, on the matrix cores
-  (``mrp_edge_logits_fwd``: 64 x 64 tiles, whole K per workgroup, bias in the epilogue; C % 32 != 0
-  or ``set_logits_path("library")`` runs ``torch.addmm`` -> hipBLASLt instead);
-* ``sigmoid``            — not run here: the aggregation kernels take the logits
-  (``MRP_AGG_GB_LOGITS``) and apply it while building their tiles.
+Both Linears run on the bf16 matrix cores at fp32 accuracy (every fp32 operand split exactly into
+three bf16 parts, six partial products; ``csrc/encoder_split.hip``), the weights split and laid out
+once per weight version (:func:`packed_weights`):
 
-Inference (no gradient wanted) runs the first two as one kernel, ``mrp_edge_encoder_fwd_split``: the
-hidden layer and the second Linear on the bf16 matrix cores at fp32 accuracy (every fp32 operand split
-exactly into three bf16 parts, six partial products; ``csrc/encoder_split.hip``), h never written.  The
-weights are split and laid out once per weight version (:func:`packed_weights`).
+* inference (no gradient wanted): ONE kernel, ``mrp_edge_encoder_fwd_split`` — h never written;
+* training (:class:`EdgeEncoderSplitFunction`, E % 32 == 0 and C % 32 == 0 — every reference
+  configuration): the same kernel also writes h^T for the backward; the backward's two GEMMs
+  (``dh^T = W2^T dz^T``, ``dW2 = dz^T h`` with db2) run on the split-bf16 weight-gradient kernel of
+  ``compress_split.hip`` on two streams, the ReLU mask, dW1 and db1 in one HIP pass.
 
-Backward (training): the two GEMMs of the second Linear (``dh = dz W2`` and ``dW2 = dz^T h``) run
-concurrently on two streams — each alone fills only part of the chip at E = 1792 — and every small
-reduction (the ReLU mask, ``dW1``, ``db1``, ``db2``) runs in one HIP pass (``mrp_edge_encoder_bwd``)
-instead of five torch launches.
+Other shapes train through :class:`EdgeEncoderFunction`: ``mrp_edge_hidden_fwd`` (K = 9, a streaming
+write) + ``mrp_edge_logits_fwd`` (fp32 MFMA, 64 x 64 tiles, bias in the epilogue; C % 32 != 0 or
+``set_logits_path("library")``: ``torch.addmm``), the backward GEMMs on torch (two streams) and the
+small reductions in one HIP pass (``mrp_edge_encoder_bwd``).
 """
 from __future__ import annotations
 

@@ -78,9 +78,9 @@ class edge_encoder(_PackedImages, nn.Module):  # noqa: N801  (reference class na
 
     def logits(self, edge: torch.Tensor) -> torch.Tensor:
         """Pre-sigmoid FiLM parameters z, (E, C, 2) interleaved.  On the GPU (``encoder.edge_logits``):
-        without a gradient, one split-bf16 matrix-core kernel for both Linears
-        (``mrp_edge_encoder_fwd_split``); with one, HIP kernels that keep the hidden layer for the
-        backward.  The sigmoid is left to the aggregation kernel (``MRP_AGG_GB_LOGITS``)."""
+        one split-bf16 matrix-core kernel for both Linears (``mrp_edge_encoder_fwd_split``); with a
+        gradient wanted the same kernel also keeps h^T for a backward on the split-bf16 GEMM kernels.
+        The sigmoid is left to the aggregation kernel (``MRP_AGG_GB_LOGITS``)."""
         if edge.is_cuda:
             z = edge_logits(self.layers, edge)
         else:
