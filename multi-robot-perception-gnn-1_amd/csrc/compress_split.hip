@@ -847,6 +847,245 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a) {
 
 __global__ void __launch_bounds__(512, 1) gemm_nt_split_w4(NTArgs a) { gemm_nt_split_body<4>(a); }
 
+// Pipelined weight-gradient form (round 4; the default where its layout conditions hold).  The NN
+// kernel's schedule (gemm_nn_split3_body) for two activation operands: 256 x 128 tiles of 8 waves of
+// 64 x 64, stages of ONE 16-k step.  Every thread's three 16-byte pieces of a stage (two A rows, one B
+// row, four k each) travel by LDS-DMA into a raw slot (two slots: stage t in slot t % 2, requested two
+// stages ahead), are read back by the same lane (its own counted vmcnt orders the read), split and
+// stored as three bf16 row images ([row][16 k], 32-byte rows, the two 16-byte chunks swapped every 8
+// rows so a fragment read meets every bank once) into a ring of three buffers (stage t in t % 3).
+// Per stage a wave waits for its own requests of stage s + 2, splits them into buffer (s + 2) % 3 —
+// which held stage s - 1, whose fragments every wave read before the barrier that ended stage s - 1 —
+// requests stage s + 4 into the slot it just read, and runs stage s's 24 MFMAs with the next stage's
+// fragments read as each fragment's last MFMA issues; one raw barrier per stage, no vmcnt(0) in the
+// loop.  LDS: 3 x 36 KiB + 2 x 24 KiB = 156 KiB.  The products and their order per output are
+// gemm_nt_split_body's: at the same split the dW outputs are bit-identical (the row sums, summed per
+// thread over other k groupings, are not).  Requires N % 16 == 0 and n0 % 16 == 0 (a wave's 16 B rows
+// lie in one source tensor).
+struct NT3 {
+  static constexpr int TM = 256, THREADS = 512, BKS = 16;
+  static constexpr int ROWB = BKS * 2;                       // bytes per [row][16 k] bf16 row
+  static constexpr int A_PART = TM * ROWB, B_PART = TN * ROWB;  // 8 KiB, 4 KiB
+  static constexpr int BUF_BYTES = 3 * (A_PART + B_PART);    // 36 KiB
+  static constexpr int NBUF = 3;
+  static constexpr int RAW_A = TM * BKS * 4;                 // 16 KiB of fp32 A pieces per stage
+  static constexpr int RAW_BYTES = RAW_A + TN * BKS * 4;     // + 8 KiB of B
+  static constexpr int RAW_OFF = NBUF * BUF_BYTES;
+  static constexpr int LDS_BYTES = RAW_OFF + 2 * RAW_BYTES;  // 156 KiB
+  static constexpr int OPS = 3;                              // LDS-DMA requests per thread per stage
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+};
+
+__device__ __forceinline__ uint32_t nt3_off(int row, int chunk) {
+  return (uint32_t)(32 * row + 16 * (chunk ^ ((row >> 3) & 1)));
+}
+
+template <int ABL = 0>  // ABL: lab ablation bits (0 in the library)
+__device__ __forceinline__ void gemm_nt_split3_body(const NTArgs& a) {
+  using G = NT3;
+  extern __shared__ u4 lds[];
+  char* ldsb = reinterpret_cast<char*>(lds);
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int tiles = a.mtiles * a.ntiles;
+  const int split = id / tiles, tid = id - split * tiles;
+  const int mt = tid % a.mtiles, nt = tid / a.mtiles;
+  const int mbase = mt * G::TM, nbase = nt * TN;
+  const int64_t kbeg = (int64_t)split * a.kchunk;
+  const int64_t kend = kbeg + a.kchunk < a.ktot ? kbeg + a.kchunk : a.ktot;
+  const int nst = kend > kbeg ? (int)((kend - kbeg) / G::BKS) : 0;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int t = threadIdx.x, qd = t & 3, r0 = t >> 2;  // k quad, row
+
+  // ---- requests: A rows r0 and r0 + 128 (rows past M clamped: any valid data, never stored), B row r0
+  uint32_t va[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    va[j] = (uint32_t)(((int64_t)min(mbase + r0 + 128 * j, a.M - 1) * a.P + 4 * qd) * 4);
+  const int nrow = min(nbase + r0, a.N - 1);
+  const bool bhi = __builtin_amdgcn_readfirstlane(nrow >= a.n0 ? 1 : 0) != 0;  // the wave's 16 rows: one side
+  const uint32_t vb = (uint32_t)(((int64_t)(bhi ? nrow - a.n0 : nrow) * a.P + 4 * qd) * 4);
+  // stages are requested in order, one at a time: the (node, pixel) of the next request is advanced
+  // incrementally (no 64-bit division per stage)
+  int64_t ind = kbeg / a.P;
+  int ipx = (int)(kbeg - ind * a.P);
+  auto issue = [&](int slot) {
+    const __amdgpu_buffer_rsrc_t ra = rsrc(a.g + ind * a.gs + ipx);
+    const __amdgpu_buffer_rsrc_t rb = rsrc(bhi ? a.s1 + ind * a.s1s + ipx : a.s0 + ind * a.s0s + ipx);
+    const int base = G::RAW_OFF + slot * G::RAW_BYTES + w * 1024;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, lds + (base + j * 8192) / 16, 16, va[j], 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, lds + (base + G::RAW_A) / 16, 16, vb, 0, 0, 0);
+    ipx += G::BKS;
+    if (ipx == a.P) {
+      ipx = 0;
+      ++ind;
+    }
+  };
+  // the raw read by inline asm (a compiler-visible read of a DMA'd location makes hipcc wait vmcnt(0)),
+  // its result guarded by an asm lgkmcnt wait naming the registers
+  const uint32_t raw_addr = (uint32_t)reinterpret_cast<uintptr_t>(ldsb + G::RAW_OFF + 16 * t);
+  struct Raw {
+    f4 v[3];
+  };
+  auto raw_read = [&](int slot) {
+    Raw r;
+    const uint32_t ad = raw_addr + (uint32_t)(slot * G::RAW_BYTES);
+    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(r.v[0]) : "v"(ad) : "memory");
+    asm volatile("ds_read_b128 %0, %1 offset:8192" : "=v"(r.v[1]) : "v"(ad) : "memory");
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r.v[2]) : "v"(ad), "i"(G::RAW_A) : "memory");
+    return r;
+  };
+  auto raw_wait = [&](Raw& r) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r.v[j])::"memory");
+  };
+  float rsum[2] = {0.f, 0.f};
+  auto put = [&](char* img, int part_bytes, int row, const f4& v) {
+    u2 p0, p1, p2;
+    f2 lo, hi;
+    lo.x = v.x, lo.y = v.y, hi.x = v.z, hi.y = v.w;
+    uint32_t l0, l1, l2, h0, h1, h2;
+    split2(lo, l0, l1, l2);
+    split2(hi, h0, h1, h2);
+    p0.x = l0, p1.x = l1, p2.x = l2, p0.y = h0, p1.y = h1, p2.y = h2;
+    const uint32_t o = nt3_off(row, qd >> 1) + 8 * (qd & 1);
+    *reinterpret_cast<u2*>(img + o) = p0;
+    *reinterpret_cast<u2*>(img + part_bytes + o) = p1;
+    *reinterpret_cast<u2*>(img + 2 * part_bytes + o) = p2;
+  };
+  auto store = [&](const Raw& r, int buf) {
+    char* base = ldsb + buf * G::BUF_BYTES;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      rsum[j] += (r.v[j].x + r.v[j].y) + (r.v[j].z + r.v[j].w);
+      put(base, G::A_PART, r0 + 128 * j, r.v[j]);
+    }
+    put(base + 3 * G::A_PART, G::B_PART, r0, r.v[2]);
+  };
+  // ---- fragments: lane (rl, hh) reads k 8 hh .. 8 hh + 7 of its row: chunk hh
+  const int hh = lane >> 5, rl = lane & 31;
+  bf8 af[2][3], bfr[2][3];
+  auto read_a = [&](int buf, int mi) {
+    const char* base = ldsb + buf * G::BUF_BYTES + nt3_off(64 * wm + 32 * mi + rl, hh);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) af[mi][p] = __builtin_bit_cast(bf8, *reinterpret_cast<const u4*>(base + p * G::A_PART));
+  };
+  auto read_b = [&](int buf, int ni) {
+    const char* base = ldsb + buf * G::BUF_BYTES + 3 * G::A_PART + nt3_off(64 * wn + 32 * ni + rl, hh);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) bfr[ni][p] = __builtin_bit_cast(bf8, *reinterpret_cast<const u4*>(base + p * G::B_PART));
+  };
+
+  Acc2 acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni].hi[r] = acc[mi][ni].lo[r] = 0.f;
+
+  if (nst > 0) {
+    // ---- prologue: stages 0 and 1 split into buffers 0 and 1, stages 2 and 3 requested
+    issue(0);
+    if (nst > 1) issue(1);
+    vm_wait<0>();
+    Raw v0 = raw_read(0);
+    raw_wait(v0);
+    store(v0, 0);
+    if (nst > 1) {
+      Raw v1 = raw_read(1);
+      raw_wait(v1);
+      store(v1, 1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (nst > 2) issue(0);
+    if (nst > 3) issue(1);
+    __builtin_amdgcn_s_barrier();
+    read_a(0, 0);
+    read_a(0, 1);
+    read_b(0, 0);
+    read_b(0, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 1
+    for (int s = 0; s < nst; ++s) {
+      const int cur = s % 3;
+      const int nxt = cur == 2 ? 0 : cur + 1;
+      const int fil = nxt == 2 ? 0 : nxt + 1;
+      const int slot = s & 1;
+      const bool have2 = s + 2 < nst;
+      // stage s + 2's requests (issued two stages ago) landed; stage s + 3's (OPS younger) may not have
+      if (s + 3 < nst)
+        vm_wait<G::OPS>();
+      else
+        vm_wait<0>();
+      // the raw read after the first MFMAs: hipcc does not count the asm reads, and its wait for this
+      // stage's first fragments would otherwise cover them too; issued here, their latency runs under
+      // those MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+      mma6(af[0], bfr[0], acc[0][0]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (have2) {
+        Raw v = raw_read(slot);
+        raw_wait(v);  // also retires the previous stage's last fragment reads
+        if (!(ABL & 8)) store(v, fil);
+      }
+      if (s + 4 < nst && !(ABL & 1)) issue(slot);  // stage s + 4, into the slot this lane's read just emptied
+      __builtin_amdgcn_sched_barrier(0);
+      mma6(af[0], bfr[1], acc[0][1]);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(nxt, 0);  // past the last stage: stale data, never used
+      __builtin_amdgcn_sched_barrier(0);
+      mma6(af[1], bfr[0], acc[1][0]);
+      __builtin_amdgcn_sched_barrier(0);
+      read_b(nxt, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma6(af[1], bfr[1], acc[1][1]);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(nxt, 1);
+      read_b(nxt, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      // every LDS operation but the 12 fragment reads just issued retired (this stage's split stores):
+      // after the barrier stage s + 2 is complete for every wave
+      asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+      if (!(ABL & 4)) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  float* out = a.out + (int64_t)split * a.M * a.N;
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int n = nbase + 64 * wn + 32 * ni + rl;
+    if (n >= a.N) continue;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mbase + 64 * wm + 32 * mi + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (m < a.M) out[(int64_t)m * a.N + n] = __fadd_rn(acc[mi][ni].hi[r], acc[mi][ni].lo[r]);
+      }
+  }
+  if (a.outb != nullptr && nt == 0) {  // the column-tile-0 workgroups write the split's row sums
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float v = rsum[j];  // the 4 threads of a row are 4 consecutive lanes (t & 3)
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      const int m = mbase + r0 + 128 * j;
+      if (qd == 0 && m < a.M) a.outb[(int64_t)split * a.M + m] = v;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(512, 1) gemm_nt_split3_w4(NTArgs a) { gemm_nt_split3_body<0>(a); }
+
 // out = sum over the splits of part (fixed order), the same for the row sums
 __global__ void __launch_bounds__(256) split_sum_nt(const f4* __restrict__ part, int nsplit, int64_t n4,
                                                     f4* __restrict__ out, const float* __restrict__ partb, int32_t M,
@@ -1001,10 +1240,22 @@ hipError_t nt_run(NTArgs a, int64_t M, int64_t N, int32_t nodes, float* out, flo
   a.N = (int32_t)N;
   const int64_t grid = (int64_t)a.mtiles * a.ntiles * ns;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split_w4),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
-  if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL(gemm_nt_split_w4, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
+  // the pipelined form where a wave's 16 B rows lie in one source tensor and the per-stage buffer
+  // offsets fit 32 bits; split_nt = 1 forces the 32-k-stage form
+  const int v = mrp_host::tuning().split_nt;
+  const bool pipelined = v != 1 && N % 16 == 0 && a.n0 % 16 == 0 &&
+                         (int64_t)M * a.P * 4 < kOffMax && (int64_t)N * a.P * 4 < kOffMax;
+  if (pipelined) {
+    static const hipError_t attr3 = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split3_w4),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, NT3::LDS_BYTES);
+    if (attr3 != hipSuccess) return attr3;
+    hipLaunchKernelGGL(gemm_nt_split3_w4, dim3((unsigned)grid), dim3(NT3::THREADS), NT3::LDS_BYTES, st, a);
+  } else {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split_w4),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(gemm_nt_split_w4, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ns == 1) return e;
   const int64_t n4 = M * N / 4;

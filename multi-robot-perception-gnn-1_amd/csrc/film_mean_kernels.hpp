@@ -722,17 +722,30 @@ __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
     if (e >= 0 && film && a.logits) w = make_float2(sigmoidf(w.x), sigmoidf(w.y));
     Wl[cl * WS + slot] = w;
   };
-  // the graph's slot sources (channel-independent), WPD words of four 8-bit sources per destination
+  // the graph's slot sources (channel-independent), WPD words of four 8-bit sources per destination;
+  // thread t builds word t (its loads issued here, ahead of the slice) and, in workgroups narrower
+  // than NT * WPD threads (one channel of a small plane), words t + blockDim.x, ... after the slice
   const bool has_word = threadIdx.x < NT * WPD;
-  int srcs[4];
-  if (has_word) {
-    const int v = threadIdx.x / WPD, q = threadIdx.x - v * WPD;
+  auto word_srcs = [&](int wi, int (&sr)[4]) {
+    const int v = wi / WPD, q = wi - v * WPD;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int jj = q * 4 + i;
-      srcs[i] = v < n && jj < K ? a.src[(node0 + v) * K + jj] - node0 : 0;
+      sr[i] = v < n && jj < K ? a.src[(node0 + v) * K + jj] - node0 : 0;
     }
-  }
+  };
+  auto pack_word = [&](const int (&sr)[4]) {
+    unsigned word = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // a source outside the graph is rejected on the host; clamp it anyway (in-bounds register index)
+      const int u = (unsigned)sr[i] < (unsigned)n ? sr[i] : 0;
+      word |= (unsigned)u << (8 * i);
+    }
+    return word;
+  };
+  int srcs[4];
+  if (has_word) word_srcs(threadIdx.x, srcs);
   int ie[IPT];  // (channel, slot) of an item are recomputed below rather than held across the slice
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
@@ -747,15 +760,11 @@ __global__ void __launch_bounds__(kBlock) film_fwd_regular(AggArgs a) {
     split_channel(a, threadIdx.x + i * blockDim.x, cl, slot);
     iw[i] = fetch_w(ie[i], cl);
   }
-  if (has_word) {
-    unsigned word = 0u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      // a source outside the graph is rejected on the host; clamp it anyway (in-bounds register index)
-      const int u = (unsigned)srcs[i] < (unsigned)n ? srcs[i] : 0;
-      word |= (unsigned)u << (8 * i);
-    }
-    slot_u[threadIdx.x] = word;
+  if (has_word) slot_u[threadIdx.x] = pack_word(srcs);
+  for (int wi = threadIdx.x + blockDim.x; wi < NT * WPD; wi += blockDim.x) {  // narrow workgroups only
+    int sr[4];
+    word_srcs(wi, sr);
+    slot_u[wi] = pack_word(sr);
   }
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {

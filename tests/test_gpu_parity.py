@@ -498,3 +498,25 @@ def test_mfma_backward_matches_valu_kernels(cuda_device, n, C, hw, knn, combine)
     dz_ref = dgb_ref * torch.sigmoid(gb) * (1 - torch.sigmoid(gb))
     assert rel_err(res[1][0].numpy(), dx_ref.numpy()) <= TOL
     assert rel_err(res[1][1].numpy(), dz_ref.numpy()) <= TOL
+
+
+@pytest.mark.parametrize("n,k,C,hw", [(5, 1, 1, (4, 4)), (16, 3, 1, (2, 2)), (9, 8, 1, (4, 4)), (16, 8, 2, (1, 4)),
+                                      (7, 5, 1, (8, 8)), (12, 2, 3, (2, 6))])
+def test_knn_narrow_workgroups(cuda_device, n, k, C, hw):
+    """k-NN graphs whose workgroups have fewer threads than the graph has destinations (one or two
+    channels of a plane of a few slices: 4-8 threads): every destination's packed slot sources must
+    still be written (found by tests/test_gpu_properties.py: n = 5, k = 1, C = 1, 4 x 4)."""
+    H, W = hw
+    g, x, gb = random_case(n, C, H, W, seed=31 * n + k, knn=k, bnn=[n, n])
+    assert g.in_degree_k() == k
+    src, dst = (t.numpy() for t in g.edges())
+    ref = oracle.film_aggregate(x, gb, src, dst).numpy()
+    out = m.film_mean(x.to(cuda_device), gb.to(cuda_device), g.csr(cuda_device)).cpu().numpy()
+    assert rel_err(out, ref) <= TOL
+    G = torch.randn_like(x)
+    dx_ref, dgb_ref = oracle.film_aggregate_grads(x, gb, src, dst, G)
+    xd = x.to(cuda_device).requires_grad_(True)
+    gbd = gb.to(cuda_device).requires_grad_(True)
+    m.film_mean(xd, gbd, g.csr(cuda_device)).backward(G.to(cuda_device))
+    assert rel_err(xd.grad.cpu().numpy(), dx_ref.numpy()) <= TOL
+    assert rel_err(gbd.grad.cpu().numpy(), dgb_ref.numpy()) <= TOL
