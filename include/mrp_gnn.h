@@ -350,8 +350,14 @@ int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const floa
  *                                      with its own workspace
  *   mrp_edge_encoder_bwd_t             dpre = dh^T (.) [h^T > 0]: dw1 (C, 9) = dpre pose, db1 (C) = row sums
  *                                      (either may be NULL); workspace: _t_workspace(E, C) bytes
- * Requirements of _bwd_split (else hipErrorNotSupported): E % 32 == 0, C % 32 == 0, 16-byte aligned
- * operands.  All sums in a fixed order: deterministic.
+ *   mrp_edge_encoder_bwd_fused         the whole backward of the encoder's parameters in four launches on
+ *                                      one stream: dz^T; dh^T and dW2 as ONE launch of both split-K
+ *                                      products; a reduction that sums their partial tiles, applies the
+ *                                      ReLU mask and forms the dW1 / db1 partials (dh^T never written);
+ *                                      their final sums.  dw1, db1, dw2, db2 all required (no dpose);
+ *                                      workspace: _fused_workspace(E, C) bytes
+ * Requirements of _bwd_split and _bwd_fused (else hipErrorNotSupported): E % 32 == 0, C % 32 == 0,
+ * 16-byte aligned operands.  All sums in a fixed order: deterministic.
  */
 int mrp_edge_encoder_fwd_split_train(const float* pose, const void* packed, const float* b2, int32_t num_edges,
                                      int32_t C, float* z, float* hT, int64_t hT_stride, void* stream);
@@ -361,6 +367,10 @@ int64_t mrp_edge_encoder_bwd_split_workspace(int32_t num_edges, int32_t C);
 int mrp_edge_encoder_bwd_split(const float* dz, const float* dzT, const float* w2T, const float* hT,
                                int32_t num_edges, int32_t C, float* dhT, float* dw2, float* db2, void* workspace,
                                int64_t workspace_bytes, void* stream);
+int64_t mrp_edge_encoder_bwd_fused_workspace(int32_t num_edges, int32_t C);
+int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, const float* hT, const float* pose,
+                               int32_t num_edges, int32_t C, float* dw1, float* db1, float* dw2, float* db2,
+                               void* workspace, int64_t workspace_bytes, void* stream);
 int64_t mrp_edge_encoder_bwd_t_workspace(int32_t num_edges, int32_t C);
 int mrp_edge_encoder_bwd_t(const float* dhT, int64_t dhT_stride, const float* hT, int64_t hT_stride,
                            const float* pose, int32_t num_edges, int32_t C, float* dw1, float* db1, void* workspace,

@@ -48,6 +48,8 @@ EXPORTED_SYMBOLS = (
     "mrp_edge_encoder_bwd_prep",
     "mrp_edge_encoder_bwd_split_workspace",
     "mrp_edge_encoder_bwd_split",
+    "mrp_edge_encoder_bwd_fused_workspace",
+    "mrp_edge_encoder_bwd_fused",
     "mrp_edge_encoder_bwd_t_workspace",
     "mrp_edge_encoder_bwd_t",
     "mrp_frame_graph_build",
@@ -152,6 +154,10 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_edge_encoder_bwd_split_workspace.restype = ctypes.c_int64
     lib.mrp_edge_encoder_bwd_split.argtypes = [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _I64, _P]
     lib.mrp_edge_encoder_bwd_split.restype = ctypes.c_int
+    lib.mrp_edge_encoder_bwd_fused_workspace.argtypes = [_I32, _I32]
+    lib.mrp_edge_encoder_bwd_fused_workspace.restype = ctypes.c_int64
+    lib.mrp_edge_encoder_bwd_fused.argtypes = [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _I64, _P]
+    lib.mrp_edge_encoder_bwd_fused.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_t_workspace.argtypes = [_I32, _I32]
     lib.mrp_edge_encoder_bwd_t_workspace.restype = ctypes.c_int64
     lib.mrp_edge_encoder_bwd_t.argtypes = [_P, _I64, _P, _I64, _P, _I32, _I32, _P, _P, _P, _I64, _P]

@@ -881,11 +881,10 @@ __device__ __forceinline__ uint32_t nt3_off(int row, int chunk) {
 }
 
 template <int ABL = 0>  // ABL: lab ablation bits (0 in the library)
-__device__ __forceinline__ void gemm_nt_split3_body(const NTArgs& a) {
+__device__ __forceinline__ void gemm_nt_split3_body(const NTArgs& a, int orig, int nwg) {
   using G = NT3;
   extern __shared__ u4 lds[];
   char* ldsb = reinterpret_cast<char*>(lds);
-  const int nwg = gridDim.x, orig = blockIdx.x;
   const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
   const int tiles = a.mtiles * a.ntiles;
@@ -1084,7 +1083,17 @@ __device__ __forceinline__ void gemm_nt_split3_body(const NTArgs& a) {
   }
 }
 
-__global__ void __launch_bounds__(512, 1) gemm_nt_split3_w4(NTArgs a) { gemm_nt_split3_body<0>(a); }
+__global__ void __launch_bounds__(512, 1) gemm_nt_split3_w4(NTArgs a) {
+  gemm_nt_split3_body<0>(a, blockIdx.x, gridDim.x);
+}
+// two independent NT products in one launch (the edge encoder's backward): workgroups [0, grid1) run
+// a1, the rest a2, each product with its own XCD-aware tile order
+__global__ void __launch_bounds__(512, 1) gemm_nt_split3_dual(NTArgs a1, NTArgs a2, int grid1) {
+  if ((int)blockIdx.x < grid1)
+    gemm_nt_split3_body<0>(a1, blockIdx.x, grid1);
+  else
+    gemm_nt_split3_body<0>(a2, blockIdx.x - grid1, gridDim.x - grid1);
+}
 
 // out = sum over the splits of part (fixed order), the same for the row sums
 __global__ void __launch_bounds__(256) split_sum_nt(const f4* __restrict__ part, int nsplit, int64_t n4,
@@ -1351,4 +1360,222 @@ extern "C" int mrp_edge_encoder_bwd_split(const float* dz, const float* dzT, con
     return nt_run(a, C2, C, 1, dw2, db2, workspace, workspace_bytes, st);  // row sums of dz^T = db2
   }
   return hipSuccess;
+}
+
+// ------------------------------------------------------------------------------------------------
+// The edge encoder's whole backward in four launches on one stream (training path, encoder.py):
+//   1. dz^T                                     (mrp_edge_encoder_bwd_prep)
+//   2. dh^T = W2^T dz^T and dW2 = dz^T h        one launch of both split-K NT products, splits chosen
+//                                               jointly so the two fill one round of the chip
+//   3. encoder_bwd_reduce: dW2 and db2 = the fixed-order sums of their partial tiles / row sums; and,
+//      per (4 hidden units, 256 edges), dh^T summed from its partial tiles, masked by [h^T > 0]
+//      (ReLU) and reduced against the block's pose rows into dW1 / db1 partials — dh^T never written
+//   4. encoder_bwd_t_final_f: the dW1 / db1 partials summed over the edge blocks in order
+// ------------------------------------------------------------------------------------------------
+namespace mrp_cs {
+
+constexpr int kNin = 9, kBtE = 256;
+
+struct EncPlan {
+  int s1, s2;
+  int64_t kc1, kc2;
+  int t1, t2;  // tiles of each product
+  int64_t off_dzT, off_p1, off_p2, off_p2b, off_t, bytes;
+};
+
+EncPlan enc_plan(int64_t E, int64_t C) {
+  EncPlan pl{};
+  const int64_t C2 = 2 * C;
+  pl.t1 = (int)(((C + NT3::TM - 1) / NT3::TM) * ((E + TN - 1) / TN));       // dh^T: M = C, N = E
+  pl.t2 = (int)(((C2 + NT3::TM - 1) / NT3::TM) * ((C + TN - 1) / TN));      // dW2: M = 2C, N = C
+  const int64_t st1 = C2 / BK, st2 = E / BK;                                // 32-k split granules
+  double best = 1e300;
+  for (int a = 1; a <= 64; ++a)
+    for (int b = 1; b <= 64; ++b) {
+      if ((int64_t)a * pl.t1 + (int64_t)b * pl.t2 > 256) continue;  // one round of one workgroup per CU
+      const int64_t p1 = (st1 + a - 1) / a, p2 = (st2 + b - 1) / b;
+      if ((st1 + p1 - 1) / p1 != a || (st2 + p2 - 1) / p2 != b) continue;  // no empty split
+      // the longer split's stages at ~1.6 us per 32 k, plus the partial tiles written and read back at ~4 TB/s
+      const double cost = (double)(p1 > p2 ? p1 : p2) * 1.6 + ((double)a * C * E + (double)b * C2 * C) * 8.0 / 4.0e6;
+      if (cost < best) {
+        best = cost;
+        pl.s1 = a;
+        pl.s2 = b;
+      }
+    }
+  if (best >= 1e300) pl.s1 = pl.s2 = 1;  // more tiles than CUs: no split
+  pl.kc1 = ((st1 + pl.s1 - 1) / pl.s1) * BK;
+  pl.kc2 = ((st2 + pl.s2 - 1) / pl.s2) * BK;
+  auto al = [](int64_t v) { return (v + 63) / 64 * 64; };  // 256-byte segments
+  int64_t o = 0;
+  pl.off_dzT = o;
+  o += al(C2 * E);
+  pl.off_p1 = o;
+  o += al((int64_t)pl.s1 * C * E);
+  pl.off_p2 = o;
+  o += al((int64_t)pl.s2 * C2 * C);
+  pl.off_p2b = o;
+  o += al((int64_t)pl.s2 * C2);
+  pl.off_t = o;
+  o += al(((E + kBtE - 1) / kBtE) * C * (kNin + 1));
+  pl.bytes = o * 4;
+  return pl;
+}
+
+// blocks [0, nb1): (4 hidden units, 256 edges) of dh^T -> dW1/db1 partials; blocks [nb1, ...): 1024
+// outputs of dW2 each (and, in the first 2C / 256 of them, 256 of db2)
+__global__ void __launch_bounds__(256) encoder_bwd_reduce(const float* __restrict__ p1, int s1,
+                                                          const float* __restrict__ hT, const float* __restrict__ pose,
+                                                          int E, int C, float* __restrict__ tpart, int nb1,
+                                                          const f4* __restrict__ p2, const float* __restrict__ p2b,
+                                                          int s2, f4* __restrict__ dw2, float* __restrict__ db2) {
+  __shared__ float ps[kBtE * kNin];
+  const int neb = (E + kBtE - 1) / kBtE;
+  if ((int)blockIdx.x < nb1) {
+    const int ug = blockIdx.x / neb, eb = blockIdx.x - ug * neb, ebase = eb * kBtE;
+    const int nrow = E - ebase < kBtE ? E - ebase : kBtE;
+    for (int i = threadIdx.x; i < nrow * kNin; i += 256) ps[i] = pose[(int64_t)ebase * kNin + i];
+    __syncthreads();
+    const int u = ug * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (u >= C) return;
+    const int64_t plane = (int64_t)C * E;
+    float acc[kNin + 1];
+#pragma unroll
+    for (int i = 0; i <= kNin; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int it = 0; it < kBtE / 64; ++it) {
+      const int el = lane + 64 * it;
+      if (el >= nrow) continue;
+      const int64_t o = (int64_t)u * E + ebase + el;
+      float dh = p1[o];
+      for (int sp = 1; sp < s1; ++sp) dh += p1[(int64_t)sp * plane + o];
+      const float d = hT[o] > 0.f ? dh : 0.f;
+#pragma unroll
+      for (int i = 0; i < kNin; ++i) acc[i] = fmaf(d, ps[el * kNin + i], acc[i]);
+      acc[kNin] += d;
+    }
+#pragma unroll
+    for (int i = 0; i <= kNin; ++i)
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) acc[i] += __shfl_xor(acc[i], o, 64);
+    if (lane <= kNin) {
+      float v = acc[0];
+#pragma unroll
+      for (int i = 1; i <= kNin; ++i) v = lane == i ? acc[i] : v;
+      tpart[((int64_t)eb * C + u) * (kNin + 1) + lane] = v;
+    }
+    return;
+  }
+  const int b = blockIdx.x - nb1;
+  const int64_t n4 = (int64_t)2 * C * C / 4;
+  const int64_t e4 = (int64_t)b * 256 + threadIdx.x;
+  if (e4 < n4) {
+    f4 v = p2[e4];
+    for (int sp = 1; sp < s2; ++sp) v += p2[(int64_t)sp * n4 + e4];
+    dw2[e4] = v;
+  }
+  const int64_t m = (int64_t)b * 256 + threadIdx.x;
+  if (m < 2 * C) {
+    float v = p2b[m];
+    for (int sp = 1; sp < s2; ++sp) v += p2b[(int64_t)sp * 2 * C + m];
+    db2[m] = v;
+  }
+}
+
+__global__ void __launch_bounds__(256) encoder_bwd_t_final_f(const float* __restrict__ part, int neb, int C,
+                                                             float* __restrict__ dw1, float* __restrict__ db1) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= C * (kNin + 1)) return;
+  float s = 0.f;
+  for (int b = 0; b < neb; ++b) s += part[(int64_t)b * C * (kNin + 1) + t];
+  const int k = t / (kNin + 1), i = t - k * (kNin + 1);
+  if (i < kNin)
+    dw1[(int64_t)k * kNin + i] = s;
+  else
+    db1[k] = s;
+}
+
+}  // namespace mrp_cs
+
+extern "C" int64_t mrp_edge_encoder_bwd_fused_workspace(int32_t num_edges, int32_t C) {
+  if (num_edges <= 0 || C <= 0 || num_edges % BK != 0 || C % 32 != 0) return 0;
+  return mrp_cs::enc_plan(num_edges, C).bytes;
+}
+
+extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, const float* hT, const float* pose,
+                                          int32_t num_edges, int32_t C, float* dw1, float* db1, float* dw2,
+                                          float* db2, void* workspace, int64_t workspace_bytes, void* stream) {
+  using namespace mrp_cs;
+  if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
+  if (C == 0) return hipSuccess;
+  if (!dw1 || !db1 || !dw2 || !db2) return hipErrorInvalidValue;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t E = num_edges, C2 = 2 * (int64_t)C;
+  if (E == 0) {  // empty sums
+    if (hipMemsetAsync(dw1, 0, (size_t)C * kNin * 4, st) != hipSuccess ||
+        hipMemsetAsync(db1, 0, (size_t)C * 4, st) != hipSuccess ||
+        hipMemsetAsync(dw2, 0, (size_t)C2 * C * 4, st) != hipSuccess || hipMemsetAsync(db2, 0, (size_t)C2 * 4, st) != hipSuccess)
+      return hipErrorUnknown;
+    return hipSuccess;
+  }
+  if (E % BK != 0 || C % 32 != 0) return hipErrorNotSupported;
+  if (!dz || !w2T || !hT || !pose || !aligned16(dz) || !aligned16(w2T) || !aligned16(hT) || !aligned16(dw2))
+    return hipErrorInvalidValue;
+  const EncPlan pl = enc_plan(E, C);
+  if (workspace == nullptr || !aligned16(workspace) || workspace_bytes < pl.bytes) return hipErrorInvalidValue;
+  float* ws = static_cast<float*>(workspace);
+  float* dzT = ws + pl.off_dzT;
+  hipError_t e = (hipError_t)mrp_edge_encoder_bwd_prep(dz, num_edges, C, dzT, E, stream);
+  if (e != hipSuccess) return e;
+  NTArgs a1 = {};  // dh^T (C x E) = W2^T (C x 2C) . dz^T: rows u, k = j
+  a1.g = w2T;
+  a1.gs = C * C2;
+  a1.s0 = dz;
+  a1.s0s = E * C2;
+  a1.s1 = dz;
+  a1.s1s = E * C2;
+  a1.n0 = (int32_t)E;
+  a1.P = (int32_t)C2;
+  a1.out = ws + pl.off_p1;
+  a1.outb = nullptr;
+  a1.ktot = C2;
+  a1.kchunk = pl.kc1;
+  a1.M = C;
+  a1.N = (int32_t)E;
+  a1.mtiles = (int32_t)((C + NT3::TM - 1) / NT3::TM);
+  a1.ntiles = (int32_t)((E + TN - 1) / TN);
+  NTArgs a2 = {};  // dW2 (2C x C) = dz^T (2C x E) . h: rows j, k = e; row sums = db2
+  a2.g = dzT;
+  a2.gs = C2 * E;
+  a2.s0 = hT;
+  a2.s0s = (int64_t)C * E;
+  a2.s1 = hT;
+  a2.s1s = (int64_t)C * E;
+  a2.n0 = C;
+  a2.P = (int32_t)E;
+  a2.out = ws + pl.off_p2;
+  a2.outb = ws + pl.off_p2b;
+  a2.ktot = E;
+  a2.kchunk = pl.kc2;
+  a2.M = (int32_t)C2;
+  a2.N = C;
+  a2.mtiles = (int32_t)((C2 + NT3::TM - 1) / NT3::TM);
+  a2.ntiles = (int32_t)((C + TN - 1) / TN);
+  const int grid1 = pl.t1 * pl.s1, grid2 = pl.t2 * pl.s2;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split3_dual),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, NT3::LDS_BYTES);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(gemm_nt_split3_dual, dim3((unsigned)(grid1 + grid2)), dim3(NT3::THREADS), NT3::LDS_BYTES, st, a1,
+                     a2, grid1);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const int neb = (int)((E + kBtE - 1) / kBtE);
+  const int nb1 = ((C + 3) / 4) * neb;
+  const int64_t nb2 = (C2 * C / 4 + 255) / 256;  // >= 2C / 256 blocks: db2 rides along
+  hipLaunchKernelGGL(encoder_bwd_reduce, dim3((unsigned)(nb1 + nb2)), dim3(256), 0, st, ws + pl.off_p1, pl.s1, hT, pose,
+                     num_edges, C, ws + pl.off_t, nb1, reinterpret_cast<const f4*>(ws + pl.off_p2), ws + pl.off_p2b,
+                     pl.s2, reinterpret_cast<f4*>(dw2), db2);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(encoder_bwd_t_final_f, dim3((unsigned)((C * (kNin + 1) + 255) / 256)), dim3(256), 0, st,
+                     ws + pl.off_t, neb, C, dw1, db1);
+  return hipGetLastError();
 }

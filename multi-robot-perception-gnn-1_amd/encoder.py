@@ -258,6 +258,15 @@ PATH_COUNTS = collections.Counter()
 
 _w2t_cache = weakref.WeakKeyDictionary()
 
+#: the single-stream fused encoder backward (``mrp_edge_encoder_bwd_fused``) when every parameter
+#: gradient and no pose gradient is wanted; False: the two-stream form (A/B comparisons)
+_BWD_FUSED = True
+
+
+def set_fused_backward(on: bool) -> None:
+    global _BWD_FUSED
+    _BWD_FUSED = bool(on)
+
 
 def transposed_w2(l2: torch.nn.Linear) -> torch.Tensor:
     """W2^T (C, 2C) row-major — the dh^T GEMM's row operand — cached per weight version like the
@@ -317,6 +326,17 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
         def workspace():
             return torch.empty((nbytes + 3) // 4, device=dev) if nbytes > 0 else None
 
+        if not need[0] and need[1] and need[2] and need[3] and need[4] and _BWD_FUSED:
+            # every parameter gradient, no pose gradient (the reference's case: poses are data): the
+            # four-launch single-stream form, dh^T never materialised
+            dw1, db1 = _grad_out(w1, (C, 9), dev), _grad_out(b1, (C,), dev)
+            dw2, db2 = _grad_out(w2, (2 * C, C), dev), _grad_out(b2, (2 * C,), dev)
+            wsf = torch.empty((int(lib.mrp_edge_encoder_bwd_fused_workspace(E, C)) + 3) // 4, device=dev)
+            with torch.cuda.device(dev):
+                _lib.check(lib.mrp_edge_encoder_bwd_fused(
+                    _ptr(dz), _ptr(w2t), _ptr(hT), _ptr(pose), E, C, _ptr(dw1), _ptr(db1), _ptr(dw2), _ptr(db2),
+                    _ptr(wsf), wsf.numel() * 4, ctypes.c_void_p(cur.cuda_stream)), "mrp_edge_encoder_bwd_fused")
+            return None, dw1, db1, dw2, db2, None, None
         dw2 = db2 = side = None
         with torch.cuda.device(dev):
             if need[3] or need[4]:  # dz^T, then dW2 = dz^T h with db2 as its row sums, on the side stream

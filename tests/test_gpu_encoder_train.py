@@ -21,11 +21,24 @@ def _reference(enc, pose, gz, dtype):
     return z.detach(), [p.grad for p in ps], pz.grad
 
 
+@pytest.mark.parametrize("form", ["fused", "two_stream", "pose_grad"])
 @pytest.mark.parametrize("E,C", [(1792, 512), (448, 2048), (512, 1024), (96, 64), (32, 32), (224, 160)])
-def test_split_training_encoder_vs_float64(cuda_device, E, C):
+def test_split_training_encoder_vs_float64(cuda_device, E, C, form):
+    """form: "fused" — parameters only, the four-launch single-stream backward
+    (``mrp_edge_encoder_bwd_fused``); "two_stream" — the same with the fused form switched off
+    (``_bwd_prep`` / ``_bwd_split`` on two streams / ``_bwd_t``); "pose_grad" — the pose needs a gradient
+    too, which only the two-stream form provides."""
+    m.encoder.set_fused_backward(form != "two_stream")
+    try:
+        _check_training_encoder(cuda_device, E, C, pose_grad=form == "pose_grad")
+    finally:
+        m.encoder.set_fused_backward(True)
+
+
+def _check_training_encoder(cuda_device, E, C, pose_grad):
     torch.manual_seed(E + 7 * C)
     enc = m.edge_encoder([C, C]).to(cuda_device)
-    pose = (torch.randn(E, 9) * 8).to(cuda_device).requires_grad_(True)
+    pose = (torch.randn(E, 9) * 8).to(cuda_device).requires_grad_(pose_grad)
     gz = torch.randn(E, 2 * C, device=cuda_device)
     before = m.encoder.PATH_COUNTS["split_train"]
     z = m.encoder.edge_logits(enc.layers, pose)
@@ -38,8 +51,28 @@ def test_split_training_encoder_vs_float64(cuda_device, E, C):
     for name, p, a32, a64 in zip(("w1", "b1", "w2", "b2"), enc.parameters(), g32, g64):
         ok, errs = stack_ref.within(p.grad, a32, a64)
         assert ok, (name, errs)
-    ok, errs = stack_ref.within(pose.grad, p32, p64)
-    assert ok, ("pose", errs)
+    if pose_grad:
+        ok, errs = stack_ref.within(pose.grad, p32, p64)
+        assert ok, ("pose", errs)
+
+
+def test_fused_and_two_stream_backward_agree(cuda_device):
+    """The fused backward and the two-stream one compute the same products in the same order per
+    output except for their split-K counts: dW1/db1/dW2/db2 agree to fp32 rounding."""
+    torch.manual_seed(5)
+    E, C = 1792, 512
+    enc = m.edge_encoder([C, C]).to(cuda_device)
+    pose = (torch.randn(E, 9) * 8).to(cuda_device)
+    gz = torch.randn(E, 2 * C, device=cuda_device)
+    grads = []
+    for fused in (True, False):
+        m.encoder.set_fused_backward(fused)
+        enc.zero_grad(set_to_none=True)
+        m.encoder.edge_logits(enc.layers, pose).backward(gz)
+        grads.append([p.grad.clone() for p in enc.parameters()])
+    m.encoder.set_fused_backward(True)
+    for a, b in zip(*grads):
+        assert float((a - b).abs().max() / b.abs().max()) < 1e-5
 
 
 def test_split_training_encoder_deterministic_and_repacks(cuda_device):

@@ -1,7 +1,8 @@
 """Kernel lab (not product code): the headline training step (bench.train_step_time's step: one GCN
 layer, B = 32 complete 8-robot graphs, C = 512, 32 x 32, forward + backward) with the encoder's
-training path on the split-bf16 kernels ("split") and on hidden + fp32-MFMA logits + hipBLASLt
-("hip"); wall time per step and the GPU time of the step's stream (events).
+training path on the split-bf16 kernels with the fused single-stream backward ("fused") or the
+two-stream one ("split2s"), and on hidden + fp32-MFMA logits + hipBLASLt ("hip"); wall time per step
+and the GPU time of the step's stream (events).
 usage: python tools/exp_headline_train.py [steps]"""
 import os
 import sys
@@ -32,8 +33,9 @@ def step():
     gcn(g, xr).backward(grad)
 
 
-for path in ("split", "hip", "split", "hip"):
-    mrp.encoder.set_logits_path(path)
+for path in ("fused", "split2s", "hip", "fused", "split2s", "hip"):
+    mrp.encoder.set_logits_path("hip" if path == "hip" else "split")
+    mrp.encoder.set_fused_backward(path == "fused")
     for _ in range(5):
         step()
     torch.cuda.synchronize()
@@ -52,6 +54,7 @@ for path in ("split", "hip", "split", "hip"):
         step()
     host = (time.perf_counter() - t1) / 10
     torch.cuda.synchronize()
-    print(f"{path:6s} wall {wall * 1e3:.3f} ms  events {e0.elapsed_time(e1) / steps:.3f} ms  host enqueue {host * 1e3:.3f} ms",
+    print(f"{path:8s} wall {wall * 1e3:.3f} ms  events {e0.elapsed_time(e1) / steps:.3f} ms  host enqueue {host * 1e3:.3f} ms",
           flush=True)
 mrp.encoder.set_logits_path("split")
+mrp.encoder.set_fused_backward(True)
