@@ -435,6 +435,7 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
   const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
   const int eb = id % eblocks, cg = id / eblocks;
+  const int ngroups = (ncb + CPG - 1) / CPG;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hh = lane >> 5;
@@ -492,9 +493,11 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) X[i] = 0.f;
     if (!(ABL & 2)) X = mma6(wa, pp, X);
-    // training: the first column group writes h^T (register i of lane (r, hh) is unit (i & 3) + 8 (i >> 2)
-    // + 4 hh of the block, edge e0 + r: each register's 32 lanes store 128 contiguous bytes of a row)
-    if (a.hT != nullptr && cg == 0 && hbx < HB && e0 + r < a.E) {
+    // training: h^T written by one workgroup per (edge block, hidden block) — every column group computes
+    // every X of its edge block, so the column groups take the hidden blocks round robin and share the
+    // stores (register i of lane (r, hh) is unit (i & 3) + 8 (i >> 2) + 4 hh of the block, edge e0 + r:
+    // each register's 32 lanes store 128 contiguous bytes of a row)
+    if (a.hT != nullptr && hbx % ngroups == cg && hbx < HB && e0 + r < a.E) {
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         a.hT[(int64_t)(hbx * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh) * a.hts + e0 + r] = relu(X[i]);
