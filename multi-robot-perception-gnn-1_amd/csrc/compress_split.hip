@@ -1447,8 +1447,18 @@ __global__ void __launch_bounds__(256) encoder_bwd_reduce(const float* __restric
       const int el = lane + 64 * it;
       if (el >= nrow) continue;
       const int64_t o = (int64_t)u * E + ebase + el;
-      float dh = p1[o];
-      for (int sp = 1; sp < s1; ++sp) dh += p1[(int64_t)sp * plane + o];
+      float dh;
+      if (s1 <= 8) {  // every partial's load issued before the sums (clamped index, no branch per load)
+        float pv[8];
+#pragma unroll
+        for (int sp = 0; sp < 8; ++sp) pv[sp] = p1[(int64_t)(sp < s1 ? sp : s1 - 1) * plane + o];
+        dh = pv[0];
+#pragma unroll
+        for (int sp = 1; sp < 8; ++sp) dh = sp < s1 ? dh + pv[sp] : dh;
+      } else {
+        dh = p1[o];
+        for (int sp = 1; sp < s1; ++sp) dh += p1[(int64_t)sp * plane + o];
+      }
       const float d = hT[o] > 0.f ? dh : 0.f;
 #pragma unroll
       for (int i = 0; i < kNin; ++i) acc[i] = fmaf(d, ps[el * kNin + i], acc[i]);
@@ -1470,8 +1480,18 @@ __global__ void __launch_bounds__(256) encoder_bwd_reduce(const float* __restric
   const int64_t n4 = (int64_t)2 * C * C / 4;
   const int64_t e4 = (int64_t)b * 256 + threadIdx.x;
   if (e4 < n4) {
-    f4 v = p2[e4];
-    for (int sp = 1; sp < s2; ++sp) v += p2[(int64_t)sp * n4 + e4];
+    f4 v;
+    if (s2 <= 8) {
+      f4 pv[8];
+#pragma unroll
+      for (int sp = 0; sp < 8; ++sp) pv[sp] = p2[(int64_t)(sp < s2 ? sp : s2 - 1) * n4 + e4];
+      v = pv[0];
+#pragma unroll
+      for (int sp = 1; sp < 8; ++sp) v = sp < s2 ? v + pv[sp] : v;
+    } else {
+      v = p2[e4];
+      for (int sp = 1; sp < s2; ++sp) v += p2[(int64_t)sp * n4 + e4];
+    }
     dw2[e4] = v;
   }
   const int64_t m = (int64_t)b * 256 + threadIdx.x;
