@@ -1390,20 +1390,22 @@ EncPlan enc_plan(int64_t E, int64_t C) {
   pl.t2 = (int)(((C2 + NT3::TM - 1) / NT3::TM) * ((C + TN - 1) / TN));      // dW2: M = 2C, N = C
   const int64_t st1 = C2 / BK, st2 = E / BK;                                // 32-k split granules
   double best = 1e300;
+  pl.s1 = pl.s2 = 1;
   for (int a = 1; a <= 64; ++a)
     for (int b = 1; b <= 64; ++b) {
-      if ((int64_t)a * pl.t1 + (int64_t)b * pl.t2 > 256) continue;  // one round of one workgroup per CU
       const int64_t p1 = (st1 + a - 1) / a, p2 = (st2 + b - 1) / b;
       if ((st1 + p1 - 1) / p1 != a || (st2 + p2 - 1) / p2 != b) continue;  // no empty split
-      // the longer split's stages at ~1.6 us per 32 k, plus the partial tiles written and read back at ~4 TB/s
-      const double cost = (double)(p1 > p2 ? p1 : p2) * 1.6 + ((double)a * C * E + (double)b * C2 * C) * 8.0 / 4.0e6;
+      // rounds of one workgroup per CU, each as long as the longer split (~1.6 us per 32 k), plus the
+      // partial tiles written and read back at ~4 TB/s
+      const int64_t rounds = ((int64_t)a * pl.t1 + (int64_t)b * pl.t2 + 255) / 256;
+      const double cost = (double)rounds * (double)(p1 > p2 ? p1 : p2) * 1.6 +
+                          ((double)a * C * E + (double)b * C2 * C) * 8.0 / 4.0e6;
       if (cost < best) {
         best = cost;
         pl.s1 = a;
         pl.s2 = b;
       }
     }
-  if (best >= 1e300) pl.s1 = pl.s2 = 1;  // more tiles than CUs: no split
   pl.kc1 = ((st1 + pl.s1 - 1) / pl.s1) * BK;
   pl.kc2 = ((st2 + pl.s2 - 1) / pl.s2) * BK;
   auto al = [](int64_t v) { return (v + 63) / 64 * 64; };  // 256-byte segments
