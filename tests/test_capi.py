@@ -131,6 +131,38 @@ def test_split_encoder_validation_without_launch():
     assert lib.mrp_edge_encoder_pack(None, None, None, 13344, None, None) == HIP_INVALID_VALUE  # size ok, no pointers
 
 
+def test_split_encoder_training_validation_without_launch():
+    """The encoder's split-bf16 training entry points (ABI 17): shape/pointer checks and workspace
+    queries on the host, before any launch (no GPU needed)."""
+    lib = m.load_library()
+    NS = m._lib.HIP_ERROR_NOT_SUPPORTED
+    # forward with h^T: declined shapes, missing pointers
+    assert lib.mrp_edge_encoder_fwd_split_train(None, None, None, 10, 48, None, None, 10, None) == NS
+    assert lib.mrp_edge_encoder_fwd_split_train(None, None, None, 32, 64, None, None, 32, None) == HIP_INVALID_VALUE
+    # dz^T: E % 4 and odd C declined; a short row stride is invalid
+    assert lib.mrp_edge_encoder_bwd_prep(16, 6, 64, 16, 6, None) == NS
+    assert lib.mrp_edge_encoder_bwd_prep(16, 8, 64, 16, 4, None) == HIP_INVALID_VALUE
+    assert lib.mrp_edge_encoder_bwd_prep(None, 0, 64, None, 0, None) == 0  # no edges: no-op
+    # the two products: E % 32 and C % 32; db2 needs the dW2 product
+    assert lib.mrp_edge_encoder_bwd_split_workspace(1792, 512) > 0
+    assert lib.mrp_edge_encoder_bwd_split_workspace(100, 512) == 0
+    assert lib.mrp_edge_encoder_bwd_split(None, None, None, None, 100, 64, 16, None, None, None, 0, None) == NS
+    assert lib.mrp_edge_encoder_bwd_split(None, None, None, None, 96, 64, None, None, 16, None, 0, None) == \
+        HIP_INVALID_VALUE
+    # ReLU mask + dW1/db1: workspace = 256-edge blocks x C x 10 floats
+    assert lib.mrp_edge_encoder_bwd_t_workspace(1792, 512) == 7 * 512 * 10 * 4
+    assert lib.mrp_edge_encoder_bwd_t(None, 0, None, 0, None, 96, 64, None, None, None, 0, None) == 0  # nothing wanted
+    assert lib.mrp_edge_encoder_bwd_t(None, 96, None, 96, None, 96, 64, 16, None, None, 0, None) == HIP_INVALID_VALUE
+    # the fused four-launch backward: all four gradients required, workspace sized by its plan
+    ws = lib.mrp_edge_encoder_bwd_fused_workspace(1792, 512)
+    assert ws >= (2 * 512 * 1792 + 7 * 512 * 10) * 4  # at least dz^T and the dW1/db1 partials
+    assert lib.mrp_edge_encoder_bwd_fused_workspace(100, 512) == 0
+    assert lib.mrp_edge_encoder_bwd_fused(None, None, None, None, 96, 64, None, None, None, None, None, 0, None) == \
+        HIP_INVALID_VALUE
+    assert lib.mrp_edge_encoder_bwd_fused(16, 16, 16, 16, 100, 64, 16, 16, 16, 16, None, 0, None) == NS
+    assert lib.mrp_edge_encoder_bwd_fused(16, 16, 16, 16, 96, 64, 16, 16, 16, 16, None, 0, None) == HIP_INVALID_VALUE
+
+
 def test_split_compress_validation_without_launch():
     lib = m.load_library()
     assert lib.mrp_compress_split_pack_bytes(512, 1024) == 512 * 1024 * 6
