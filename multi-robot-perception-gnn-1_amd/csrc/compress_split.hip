@@ -1005,10 +1005,16 @@ __device__ __forceinline__ void gemm_nt_split3_body(const NTArgs& a, int orig, i
     if (nst > 2) issue(0);
     if (nst > 3) issue(1);
     __builtin_amdgcn_s_barrier();
+    // the loop's read order (A block 0, B block 0, A block 1, B block 1): hipcc's wait before the first
+    // MFMAs of a stage merges the states of both paths into the loop
+    __builtin_amdgcn_sched_barrier(0);
     read_a(0, 0);
-    read_a(0, 1);
+    __builtin_amdgcn_sched_barrier(0);
     read_b(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(0, 1);
     read_b(0, 1);
+    __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll 1
