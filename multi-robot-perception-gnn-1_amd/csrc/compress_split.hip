@@ -701,12 +701,28 @@ __device__ __forceinline__ uint32_t rowoff(int row, int chunk) {  // [row][4 chu
   return (uint32_t)(64 * row + 16 * (chunk ^ ((row >> 2) & 3)));
 }
 
-template <int WMW>
-__device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a) {
+// 16x16x32 form of the six partial products (four accumulator registers per 16 x 16 tile)
+typedef float f4acc __attribute__((ext_vector_type(4)));
+struct Acc2s {
+  f4acc hi, lo;
+};
+__device__ __forceinline__ void mma6_16(const bf8 (&a)[3], const bf8 (&b)[3], Acc2s& acc) {
+  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc.lo, 0, 0, 0);
+  acc.hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc.hi, 0, 0, 0);
+}
+
+// MF16: the products on v_mfma_f32_16x16x32_bf16 (the wave's 64 x 64 as 4 x 4 tiles of 16 x 16, one
+// MFMA per 32 k), which holds a higher clock than the 32x32x16 shape under the chip's power limit
+// (MI355X_MICROARCH.md, DVFS give-back item 7)
+template <int WMW, bool MF16 = false>
+__device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a, int orig, int nwg) {
   using G = NTGeo<WMW>;
   extern __shared__ u4 lds[];
   char* ldsb = reinterpret_cast<char*>(lds);
-  const int nwg = gridDim.x, orig = blockIdx.x;
   const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
   const int tiles = a.mtiles * a.ntiles;
@@ -791,6 +807,59 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a) {
     }
   };
 
+  if constexpr (MF16) {
+    // lane (r16, q) reads k = 8 q .. 8 q + 7 (chunk q) of row r16 of a 16-row block
+    const int r16 = lane & 15, q = lane >> 4;
+    Acc2s acc[4][4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[mi][ni].hi[r] = acc[mi][ni].lo[r] = 0.f;
+    if (nst > 0) load(0);
+#pragma unroll 1
+    for (int s = 0; s < nst; ++s) {
+      const int buf = s & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store(buf);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (s + 1 < nst) load(s + 1);
+      const char* base = ldsb + buf * G::BUF_BYTES;
+      const char* bb = base + 3 * G::A_PART;
+      bf8 bf[4][3];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bf[ni][p] = __builtin_bit_cast(bf8, *reinterpret_cast<const u4*>(bb + p * G::B_PART +
+                                                                            rowoff(64 * wn + 16 * ni + r16, q)));
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        bf8 af[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          af[p] = __builtin_bit_cast(bf8, *reinterpret_cast<const u4*>(base + p * G::A_PART +
+                                                                        rowoff(64 * wm + 16 * mi + r16, q)));
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) mma6_16(af, bf[ni], acc[mi][ni]);
+      }
+    }
+    float* out = a.out + (int64_t)split * a.M * a.N;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = nbase + 64 * wn + 16 * ni + r16;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = mbase + 64 * wm + 16 * mi + 4 * q + r;
+          if (m < a.M) out[(int64_t)m * a.N + n] = __fadd_rn(acc[mi][ni].hi[r], acc[mi][ni].lo[r]);
+        }
+    }
+  } else {
   Acc2 acc[2][2];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -832,6 +901,7 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a) {
         if (m < a.M) out[(int64_t)m * a.N + n] = __fadd_rn(acc[mi][ni].hi[r], acc[mi][ni].lo[r]);
       }
   }
+  }
   if (a.outb != nullptr && nt == 0) {  // the column-tile-0 workgroups write the split's row sums
 #pragma unroll
     for (int j = 0; j < G::AJ; ++j) {
@@ -845,7 +915,12 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a) {
   }
 }
 
-__global__ void __launch_bounds__(512, 1) gemm_nt_split_w4(NTArgs a) { gemm_nt_split_body<4>(a); }
+__global__ void __launch_bounds__(512, 1) gemm_nt_split_w4(NTArgs a) {
+  gemm_nt_split_body<4>(a, blockIdx.x, gridDim.x);
+}
+__global__ void __launch_bounds__(512, 1) gemm_nt_split_w4_mf16(NTArgs a) {
+  gemm_nt_split_body<4, true>(a, blockIdx.x, gridDim.x);
+}
 
 // Pipelined weight-gradient form (round 4; the default where its layout conditions hold).  The NN
 // kernel's schedule (gemm_nn_split3_body) for two activation operands: 256 x 128 tiles of 8 waves of
@@ -1092,13 +1167,13 @@ __device__ __forceinline__ void gemm_nt_split3_body(const NTArgs& a, int orig, i
 __global__ void __launch_bounds__(512, 1) gemm_nt_split3_w4(NTArgs a) {
   gemm_nt_split3_body<0>(a, blockIdx.x, gridDim.x);
 }
-// two independent NT products in one launch (the edge encoder's backward): workgroups [0, grid1) run
-// a1, the rest a2, each product with its own XCD-aware tile order
-__global__ void __launch_bounds__(512, 1) gemm_nt_split3_dual(NTArgs a1, NTArgs a2, int grid1) {
+// two independent NT products in one launch (the edge encoder's backward), on the default (16x16x32)
+// form: workgroups [0, grid1) run a1, the rest a2, each product with its own XCD-aware tile order
+__global__ void __launch_bounds__(512, 1) gemm_nt_dual_mf16(NTArgs a1, NTArgs a2, int grid1) {
   if ((int)blockIdx.x < grid1)
-    gemm_nt_split3_body<0>(a1, blockIdx.x, grid1);
+    gemm_nt_split_body<4, true>(a1, blockIdx.x, grid1);
   else
-    gemm_nt_split3_body<0>(a2, blockIdx.x - grid1, gridDim.x - grid1);
+    gemm_nt_split_body<4, true>(a2, blockIdx.x - grid1, gridDim.x - grid1);
 }
 
 // out = sum over the splits of part (fixed order), the same for the row sums
@@ -1255,10 +1330,24 @@ hipError_t nt_run(NTArgs a, int64_t M, int64_t N, int32_t nodes, float* out, flo
   a.N = (int32_t)N;
   const int64_t grid = (int64_t)a.mtiles * a.ntiles * ns;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  // the pipelined form where a wave's 16 B rows lie in one source tensor and the per-stage buffer
-  // offsets fit 32 bits; split_nt = 1 forces the 32-k-stage form
+  // split_nt: -1 / 3 (default) the 32-k-stage form on 16x16x32 MFMAs — 4-5 % faster than either
+  // 32x32x16 form at every config shape (tools/exp_nt_forms.py: the chip holds a higher clock for that
+  // shape under its power limit); 2 the pipelined 16-k-stage 32x32x16 form; 1 the 32-k-stage one
   const int v = mrp_host::tuning().split_nt;
-  const bool pipelined = v != 1 && N % 16 == 0 && a.n0 % 16 == 0 &&
+  if (v == 3 || v < 0) {
+    static const hipError_t attr16 = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split_w4_mf16),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+    if (attr16 != hipSuccess) return attr16;
+    hipLaunchKernelGGL(gemm_nt_split_w4_mf16, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
+    hipError_t e3 = hipGetLastError();
+    if (e3 != hipSuccess || ns == 1) return e3;
+    const int64_t n4 = M * N / 4;
+    const int64_t blocks = (n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048;
+    hipLaunchKernelGGL(split_sum_nt, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<const f4*>(ws), ns, n4,
+                       reinterpret_cast<f4*>(out), a.outb, (int32_t)M, outb);
+    return hipGetLastError();
+  }
+  const bool pipelined = v == 2 && N % 16 == 0 && a.n0 % 16 == 0 &&
                          (int64_t)M * a.P * 4 < kOffMax && (int64_t)N * a.P * 4 < kOffMax;
   if (pipelined) {
     static const hipError_t attr3 = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split3_w4),
@@ -1590,10 +1679,11 @@ extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, con
   a2.mtiles = (int32_t)((C2 + NT3::TM - 1) / NT3::TM);
   a2.ntiles = (int32_t)((C + TN - 1) / TN);
   const int grid1 = pl.t1 * pl.s1, grid2 = pl.t2 * pl.s2;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split3_dual),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, NT3::LDS_BYTES);
+  using GN = NTGeo<4>;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_dual_mf16),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, GN::LDS_BYTES);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL(gemm_nt_split3_dual, dim3((unsigned)(grid1 + grid2)), dim3(NT3::THREADS), NT3::LDS_BYTES, st, a1,
+  hipLaunchKernelGGL(gemm_nt_dual_mf16, dim3((unsigned)(grid1 + grid2)), dim3(GN::THREADS), GN::LDS_BYTES, st, a1,
                      a2, grid1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int neb = (int)((E + kBtE - 1) / kBtE);

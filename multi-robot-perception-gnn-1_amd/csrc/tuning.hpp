@@ -42,8 +42,8 @@ struct Tuning {
   // mrp_edge_encoder_fwd_split kernel: -1 per shape, 0 the per-wave hidden layer, 1..4 shared-hidden
   // forms (CB, waves) = (1, 4), (2, 4), (1, 8), (2, 8)
   int edge_split_v = -1;
-  // split-bf16 weight-gradient (NT) kernel: -1 / 2 the pipelined 16-k-stage form where its layout
-  // conditions hold (gemm_nt_split3_w4), 1 the 32-k-stage form (gemm_nt_split_w4)
+  // split-bf16 weight-gradient (NT) kernel: -1 / 3 the 32-k-stage form on 16x16x32 MFMAs (default),
+  // 2 the pipelined 16-k-stage 32x32x16 form (gemm_nt_split3_w4), 1 the 32-k-stage 32x32x16 form
   int split_nt = -1;
   int edge_gemm = 1;  // edge encoder's second Linear: 64 x 64 tiles of 32 x 32 waves on 16x16x4 (0) or 32x32x2 (1) MFMAs
 };

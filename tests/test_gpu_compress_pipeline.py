@@ -74,3 +74,38 @@ def test_config1_size_repeats_bit_identical(cuda_device, form):
             assert torch.equal(d[0], d0[0]) and torch.equal(d[1], d0[1])
             g = m.compress.compress_backward_weight(gy, x, a)
             assert torch.equal(g[0], w0[0]) and torch.equal(g[1], w0[1])
+
+
+@pytest.mark.parametrize("form", [1, 2, 3])
+@pytest.mark.parametrize("n,C,H,W", [(16, 64, 8, 8), (10, 128, 16, 16), (64, 256, 8, 8), (7, 160, 4, 8), (2, 32, 32, 32),
+                                     (33, 96, 8, 8), (8, 512, 8, 8), (3, 320, 16, 16), (128, 512, 32, 32)])
+def test_weight_gradient_forms_vs_float64(cuda_device, form, n, C, H, W):
+    """The weight gradient on each NT kernel form (split_nt 1: 32-k stages on 32x32x16 MFMAs, 2: the
+    pipelined 16-k-stage form, 3 (default): 32-k stages on 16x16x32 MFMAs) against float64 with the
+    fp32 yardstick, repeated launches bit-identical; forms 1 and 2 compute the same products in the
+    same order per output (bit-identical dW at equal splits)."""
+    import stack_ref
+    torch.manual_seed(n * 13 + C)
+    dev = cuda_device
+    x, a, gy = (torch.randn(n, C, H, W, device=dev) for _ in range(3))
+    lib = m.load_library()
+    prev = m.compress.compress_path()
+    m.compress.set_compress_path("split")
+    assert lib.mrp_tuning_set(b"split_nt", form) == 0
+    try:
+        gw, gb = m.compress.compress_backward_weight(gy, x, a)
+        again = m.compress.compress_backward_weight(gy, x, a)
+        if form == 2:
+            assert lib.mrp_tuning_set(b"split_nt", 1) == 0
+            assert torch.equal(gw, m.compress.compress_backward_weight(gy, x, a)[0])
+    finally:
+        lib.mrp_tuning_set(b"split_nt", -1)
+        m.compress.set_compress_path(prev)
+    assert torch.equal(gw, again[0]) and torch.equal(gb, again[1])
+    cat = torch.cat((x, a), 1)
+    w64 = torch.einsum("nohw,nchw->oc", gy.double(), cat.double()).reshape(C, 2 * C, 1, 1)
+    w32 = torch.einsum("nohw,nchw->oc", gy, cat).reshape(C, 2 * C, 1, 1)
+    ok, errs = stack_ref.within(gw, w32, w64)
+    assert ok, ("gw", errs)
+    ok, errs = stack_ref.within(gb, gy.sum((0, 2, 3)), gy.double().sum((0, 2, 3)))
+    assert ok, ("gb", errs)
