@@ -426,9 +426,10 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * or 8 waves with 1 or 2 column blocks each); "edge_split_cb" (form 0: 32-column
  * blocks per wave, 1 or 2; 0, default: per shape); "edge_split_k" (its hidden blocks over 1 or 2
  * wave sets, 2 only when C % 64 == 0; 0, default: per shape); "gemm_split" (split-bf16 compress
- * forward / data-gradient kernel: -1 per shape (5 where M % 256 == 0, else 2), 2 = 128 rows / 4 waves,
+ * forward / data-gradient kernel: -1 per shape (7 where M % 256 == 0, else 2), 2 = 128 rows / 4 waves,
  * 4 = 256 rows / 8 waves with 32-k stages, 5 = 256 rows / 8 waves, pipelined 16-k stages, 6 = two
- * pipelined 128-row / 4-wave workgroups per CU; any other value is rejected); "split_nt" (split-bf16
+ * pipelined 128-row / 4-wave workgroups per CU, 7 = 256 rows / 8 waves with 32-k stages on 16x16x32
+ * MFMAs; any other value is rejected); "split_nt" (split-bf16
  * weight-gradient kernel of mrp_compress_bwd_weight_split and mrp_edge_encoder_bwd_split: -1 or 3,
  * default: 32-k stages on 16x16x32 MFMAs; 2 = the pipelined 16-k-stage 32x32x16 form where its layout
  * conditions hold; 1 = 32-k stages on 32x32x16; 0 is rejected). */

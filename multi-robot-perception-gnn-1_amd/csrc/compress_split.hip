@@ -95,6 +95,20 @@ __device__ __forceinline__ void mma6(const bf8 (&a)[3], const bf8 (&b)[3], Acc2&
   acc.hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc.hi, 0, 0, 0);
 }
 
+// 16x16x32 form of the six partial products (four accumulator registers per 16 x 16 tile)
+typedef float f4acc __attribute__((ext_vector_type(4)));
+struct Acc2s {
+  f4acc hi, lo;
+};
+__device__ __forceinline__ void mma6_16(const bf8 (&a)[3], const bf8 (&b)[3], Acc2s& acc) {
+  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc.lo, 0, 0, 0);
+  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc.lo, 0, 0, 0);
+  acc.hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc.hi, 0, 0, 0);
+}
+
 // byte offset of 16-byte chunk ch (8 columns) of row `row` in a [BK][TN] bf16 image
 __device__ __forceinline__ uint32_t boff(int row, int ch) {
   return (uint32_t)(256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))));
@@ -147,7 +161,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
 
-template <int WMW>
+template <int WMW, bool MF16 = false>
 __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
   using G = Geo<WMW>;
   constexpr int TM = G::TM, NW = G::NW, A_PIECES = G::A_PIECES, A_BYTES = G::A_BYTES, BUF_BYTES = G::BUF_BYTES;
@@ -249,6 +263,103 @@ __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
       }
   };
 
+  if constexpr (MF16) {
+    // 16x16x32 products over the whole 32-k stage: lane (r16, qq) of a 16 x 16 tile holds k = 8 qq ..
+    // 8 qq + 7.  A: 16-row block mi of the wave is half (mi & 1) of 32-row block 2 wm + (mi >> 1); the
+    // packed image holds 16-k steps in the 32 x 32 x 16 lane order (lane r + 32 hh: row r, k 8 hh ..),
+    // so the lane reads step qq >> 1, slot 16 (mi & 1) + r16 + 32 (qq & 1).  B: the transposing reads of
+    // rows 8 qq + 4 t .. + 3 (t = 0, 1), columns 64 wn + 16 ni ...
+    const int r16 = lane & 15, qq = lane >> 4;
+    uint32_t tr16[4][2];  // byte address of read (ni, t) in buffer 0, part 0
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        tr16[ni][t] = (uint32_t)reinterpret_cast<uintptr_t>(
+            ldsb + A_BYTES + boff(8 * qq + 4 * t + trq, (64 * wn + 16 * ni) / 8 + (trp >> 1)) + 8 * (trp & 1));
+    const int aslot = (r16 + 32 * (qq & 1)) * 16;
+    Acc2s acc[4][4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[mi][ni].hi[r] = acc[mi][ni].lo[r] = 0.f;
+    issue_a(0, 0);
+    load_b(0);
+#pragma unroll 1
+    for (int s = 0; s < nst; ++s) {
+      const int buf = s & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store_b(buf);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // B fragments by inline-asm transposing reads (the builtin carries no memory operand: hipcc would
+      // wait for the LDS-DMA issued below, which fills the other buffer), waited for by hand
+      s4 v[4][3][2];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"
+                         : "=v"(v[ni][p][t])
+                         : "v"(tr16[ni][t] + (uint32_t)(buf * BUF_BYTES)), "i"(p * B_PART_BYTES));
+      if (s + 1 < nst) {
+        issue_a(s + 1, buf ^ 1);
+        load_b(s + 1);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bf8 bf[4][3];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          asm volatile("" : "+v"(v[ni][p][0]), "+v"(v[ni][p][1]));
+          u4 u;
+          u.x = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][0], v[ni][p][0], 0, 1));
+          u.y = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][0], v[ni][p][0], 2, 3));
+          u.z = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][1], v[ni][p][1], 0, 1));
+          u.w = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][1], v[ni][p][1], 2, 3));
+          bf[ni][p] = __builtin_bit_cast(bf8, u);
+        }
+      const char* abase = ldsb + buf * BUF_BYTES + aslot;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        bf8 af[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          af[p] = __builtin_bit_cast(
+              bf8, *reinterpret_cast<const u4*>(abase + (((2 * wm + (mi >> 1)) * 2 + (qq >> 1)) * 3 + p) * 1024 +
+                                                16 * 16 * (mi & 1)));
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) mma6_16(af, bf[ni], acc[mi][ni]);
+      }
+    }
+    // accumulator register r of lane (r16, qq) of tile (mi, ni): row 16 mi + 4 qq + r, column 16 ni + r16
+    const int mb0 = mt * TM + 64 * wm;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int64_t n = nbase + 64 * wn + 16 * ni + r16;
+      if (n >= a.ncols) continue;
+      const int64_t nd = n / a.P, px = n - nd * a.P;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = mb0 + 16 * mi + 4 * qq + r;
+          if (m >= a.M) continue;
+          float v = __fadd_rn(acc[mi][ni].hi[r], acc[mi][ni].lo[r]);
+          if (a.bias != nullptr) v = __fadd_rn(v, a.bias[m]);
+          float* dst = m < a.m0 ? a.c0 + nd * a.c0s + (int64_t)m * a.P + px
+                                : a.c1 + nd * a.c1s + (int64_t)(m - a.m0) * a.P + px;
+          *dst = v;
+        }
+    }
+    return;
+  }
+
   Acc2 acc[2][2];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -306,6 +417,7 @@ __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
 
 __global__ void __launch_bounds__(256, 1) gemm_nn_split_w2(Args a) { gemm_nn_split_body<2>(a); }
 __global__ void __launch_bounds__(512, 1) gemm_nn_split_w4(Args a) { gemm_nn_split_body<4>(a); }
+__global__ void __launch_bounds__(512, 1) gemm_nn_split_w4_mf16(Args a) { gemm_nn_split_body<4, true>(a); }
 
 // ------------------------------------------------------------------------------------------------
 // Pipelined NN form (256 x 128 tiles, 8 waves of 64 x 64): stages of ONE 16-k step in a ring of
@@ -648,16 +760,19 @@ hipError_t launch(Args a, hipStream_t st) {
   if (a.K % BK != 0 || a.k0 % BK != 0 || a.M % 32 != 0 || a.P % 4 != 0) return hipErrorNotSupported;
   if ((int64_t)a.M * a.K * 6 >= kOffMax) return hipErrorNotSupported;
   // 256-row workgroups (8 waves, two per SIMD, each B stage split once for 256 rows) when M is a
-  // multiple of 256: the pipelined form (5) by default — bit-identical to the 32-k-stage form (4), 3-11 %
-  // faster at every config shape (tools/gemm_lab.cpp: configs[3] forward 189 -> 210 TF/s) — else
-  // 128-row ones.  6 (two 4-wave workgroups per CU, pipelined) measured no faster than 4 and is a lab
-  // variant.
+  // multiple of 256, else 128-row ones.  The 256-row default is the 32-k-stage form on 16x16x32 MFMAs
+  // (7): 7-9 % faster than the pipelined 32x32x16 form (5) at every config shape (tools/exp_nn_forms.py:
+  // configs[3] forward 214 -> 232 TF/s) — the smaller MFMA holds a higher clock under the power limit.
+  // 5 is bit-identical to the 32-k-stage 32x32x16 form (4), 3-11 % faster than it; 6 (two 4-wave
+  // workgroups per CU, pipelined) measured no faster than 4.  Both are lab variants now.
   int v = mrp_host::tuning().gemm_split;
-  if (v < 0 && a.M % 256 == 0) v = 5;
+  if (v < 0 && a.M % 256 == 0) v = 7;
   if (v == 5 || v == 6) {
     const hipError_t e = v == 5 ? launch3<4, 2>(a, st, gemm_nn_split3_w4) : launch3<2, 1>(a, st, gemm_nn_split3_w2);
     if (e != hipErrorNotSupported) return e;
   }
+  if (v == 7)
+    return launch_w<4>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w4_mf16), gemm_nn_split_w4_mf16);
   const bool wide = v == 4 || (v < 0 && a.M % 256 == 0);
   return wide ? launch_w<4>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w4), gemm_nn_split_w4)
               : launch_w<2>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w2), gemm_nn_split_w2);
@@ -701,19 +816,6 @@ __device__ __forceinline__ uint32_t rowoff(int row, int chunk) {  // [row][4 chu
   return (uint32_t)(64 * row + 16 * (chunk ^ ((row >> 2) & 3)));
 }
 
-// 16x16x32 form of the six partial products (four accumulator registers per 16 x 16 tile)
-typedef float f4acc __attribute__((ext_vector_type(4)));
-struct Acc2s {
-  f4acc hi, lo;
-};
-__device__ __forceinline__ void mma6_16(const bf8 (&a)[3], const bf8 (&b)[3], Acc2s& acc) {
-  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc.lo, 0, 0, 0);
-  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc.lo, 0, 0, 0);
-  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc.lo, 0, 0, 0);
-  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc.lo, 0, 0, 0);
-  acc.lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc.lo, 0, 0, 0);
-  acc.hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc.hi, 0, 0, 0);
-}
 
 // MF16: the products on v_mfma_f32_16x16x32_bf16 (the wave's 64 x 64 as 4 x 4 tiles of 16 x 16, one
 // MFMA per 32 k), which holds a higher clock than the 32x32x16 shape under the chip's power limit

@@ -110,13 +110,13 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"edge_split_cb", &t.edge_split_cb, 0, 2},
       {"edge_split_k", &t.edge_split_k, 0, 2},
       {"edge_split_v", &t.edge_split_v, -1, 4},
-      {"gemm_split", &t.gemm_split, -1, 6},
+      {"gemm_split", &t.gemm_split, -1, 7},
       {"split_nt", &t.split_nt, -1, 3},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {
       if (value < k.lo || value > k.hi) return hipErrorInvalidValue;
-      // gemm_split names a kernel: -1 (per shape), 2, 4, 5 or 6 (compress_split.hip); no other value means one
+      // gemm_split names a kernel: -1 (per shape), 2, 4, 5, 6 or 7 (compress_split.hip); no other value means one
       if (k.field == &t.gemm_split && (value == 0 || value == 1 || value == 3)) return hipErrorInvalidValue;
       if (k.field == &t.split_nt && value == 0) return hipErrorInvalidValue;
       *k.field = value;

@@ -1,12 +1,14 @@
 """The split-bf16 compress forward / data-gradient kernel forms (``csrc/compress_split.hip``; knob
 ``gemm_split``): 2 = 128-row workgroups, 4 = 256-row with 32-k stages, 5 = the pipelined 256-row form
 (16-k stages in a ring of four LDS buffers, both operands by LDS-DMA with counted waits, the default
-where M % 256 == 0), 6 = two pipelined 128-row workgroups per CU.  All of them accumulate the same
+where M % 256 == 0 before form 7), 6 = two pipelined 128-row workgroups per CU, 7 = 256-row 32-k
+stages on 16x16x32 MFMAs (the default where M % 256 == 0).  Forms 2, 4, 5 and 6 accumulate the same
 partial products in the same k order, so their outputs must be bit-identical — across ragged M and
 column tails, the shortest K (two 16-k stages), planes smaller than a column tile — and every launch
 of one kernel must repeat the last bit for bit at a BASELINE config size (the guard against an
 LDS-DMA ordering race: a read that overtakes the DMA it depends on gives rare, shifting errors).
-Accuracy against float64 is tests/test_gpu_compress_gemm.py's."""
+Form 7 sums 32 k per MFMA instead of 16, so it is held to float64 with the fp32 yardstick here (the
+default path's accuracy is tests/test_gpu_compress_gemm.py's)."""
 import contextlib
 
 import pytest
@@ -54,7 +56,7 @@ def test_forms_bit_identical(cuda_device, n, C, H, W):
         assert torch.equal(ga, ga0), (v, float((ga - ga0).abs().max()))
 
 
-@pytest.mark.parametrize("form", [5, 6])
+@pytest.mark.parametrize("form", [5, 6, 7])
 def test_config1_size_repeats_bit_identical(cuda_device, form):
     """configs[1]'s layer shape (128 nodes, C = 512, 32 x 32): forward, data gradient and weight
     gradient launched repeatedly on the same inputs give the same bits every time."""
@@ -74,6 +76,37 @@ def test_config1_size_repeats_bit_identical(cuda_device, form):
             assert torch.equal(d[0], d0[0]) and torch.equal(d[1], d0[1])
             g = m.compress.compress_backward_weight(gy, x, a)
             assert torch.equal(g[0], w0[0]) and torch.equal(g[1], w0[1])
+
+
+@pytest.mark.parametrize("n,C,H,W", [(3, 32, 2, 2), (5, 64, 4, 4), (7, 160, 4, 8), (2, 256, 8, 8), (9, 288, 2, 6),
+                                     (33, 96, 8, 8), (4, 512, 16, 16), (1, 256, 1, 4), (17, 320, 4, 4),
+                                     (16, 1280, 8, 8)])
+def test_mf16_form_vs_float64(cuda_device, n, C, H, W):
+    """Form 7 (16x16x32 MFMAs) — the default where M % 256 == 0, forced here on every shape (ragged M
+    tiles and column tails, the shortest K, planes smaller than a column tile): forward and data
+    gradient against float64 with the fp32 yardstick, repeated launches bit-identical."""
+    import stack_ref
+    torch.manual_seed(n * 5 + C)
+    dev = cuda_device
+    w = torch.randn(C, 2 * C, 1, 1, device=dev) / (2 * C) ** 0.5
+    b = torch.randn(C, device=dev)
+    x, a, gy = (torch.randn(n, C, H, W, device=dev) for _ in range(3))
+    with _form(7):
+        y = m.compress.compress_forward(w, b, x, a)
+        gx, ga = m.compress.compress_backward_data(w, gy)
+        assert torch.equal(y, m.compress.compress_forward(w, b, x, a))
+        d = m.compress.compress_backward_data(w, gy)
+        assert torch.equal(d[0], gx) and torch.equal(d[1], ga)
+    cat = torch.cat((x, a), 1)
+    w2 = w.reshape(C, 2 * C)
+    y32 = torch.einsum("oc,nchw->nohw", w2, cat) + b.view(1, C, 1, 1)
+    y64 = torch.einsum("oc,nchw->nohw", w2.double(), cat.double()) + b.double().view(1, C, 1, 1)
+    ok, errs = stack_ref.within(y, y32, y64)
+    assert ok, ("y", errs)
+    g32 = torch.einsum("oc,nohw->nchw", w2, gy)
+    g64 = torch.einsum("oc,nohw->nchw", w2.double(), gy.double())
+    ok, errs = stack_ref.within(torch.cat((gx, ga), 1), g32, g64)
+    assert ok, ("grad", errs)
 
 
 @pytest.mark.parametrize("form", [1, 2, 3])
