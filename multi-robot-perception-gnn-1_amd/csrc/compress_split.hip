@@ -278,6 +278,8 @@ __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
         tr16[ni][t] = (uint32_t)reinterpret_cast<uintptr_t>(
             ldsb + A_BYTES + boff(8 * qq + 4 * t + trq, (64 * wn + 16 * ni) / 8 + (trp >> 1)) + 8 * (trp & 1));
     const int aslot = (r16 + 32 * (qq & 1)) * 16;
+    const uint32_t abase0 =
+        (uint32_t)reinterpret_cast<uintptr_t>(ldsb + aslot + ((4 * wm + (qq >> 1)) * 3) * 1024);
     Acc2s acc[4][4];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -294,47 +296,75 @@ __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
       store_b(buf);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      // B fragments by inline-asm transposing reads (the builtin carries no memory operand: hipcc would
-      // wait for the LDS-DMA issued below, which fills the other buffer), waited for by hand
-      s4 v[4][3][2];
+      {  // (scope of the stage's fragments)
+        // every fragment read by inline asm (the transposing-read builtin carries no memory operand, so
+        // hipcc would wait for the LDS-DMA issued below, which fills the other buffer) with counted
+        // waits, in the order the MFMAs need them: A row 0, B columns 0..3, then A row mi + 1 under row
+        // mi's MFMAs (lgkmcnt holds at most 15).  2-3 % over one wait for all of them.
+        const uint32_t ab = abase0 + (uint32_t)(buf * BUF_BYTES);
+        u4 ar[2][3];
+        s4 v[4][3][2];
+        auto read_a16 = [&](int mi, u4 (&r)[3]) {
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
+          for (int p = 0; p < 3; ++p)
+            asm volatile("ds_read_b128 %0, %1 offset:%2"
+                         : "=v"(r[p])
+                         : "v"(ab), "i"((mi >> 1) * 6144 + p * 1024 + 256 * (mi & 1)));
+        };
+        read_a16(0, ar[0]);
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
-            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"
-                         : "=v"(v[ni][p][t])
-                         : "v"(tr16[ni][t] + (uint32_t)(buf * BUF_BYTES)), "i"(p * B_PART_BYTES));
-      if (s + 1 < nst) {
-        issue_a(s + 1, buf ^ 1);
-        load_b(s + 1);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      bf8 bf[4][3];
+          for (int p = 0; p < 3; ++p)
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          asm volatile("" : "+v"(v[ni][p][0]), "+v"(v[ni][p][1]));
-          u4 u;
-          u.x = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][0], v[ni][p][0], 0, 1));
-          u.y = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][0], v[ni][p][0], 2, 3));
-          u.z = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][1], v[ni][p][1], 0, 1));
-          u.w = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][1], v[ni][p][1], 2, 3));
-          bf[ni][p] = __builtin_bit_cast(bf8, u);
+            for (int t = 0; t < 2; ++t)
+              asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"
+                           : "=v"(v[ni][p][t])
+                           : "v"(tr16[ni][t] + (uint32_t)(buf * BUF_BYTES)), "i"(p * B_PART_BYTES));
+        if (s + 1 < nst) {
+          issue_a(s + 1, buf ^ 1);
+          load_b(s + 1);
         }
-      const char* abase = ldsb + buf * BUF_BYTES + aslot;
+        bf8 bf[4][3];
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        bf8 af[3];
+        for (int mi = 0; mi < 4; ++mi) {
+          u4 (&cur)[3] = ar[mi & 1];
+          if (mi < 3) read_a16(mi + 1, ar[(mi + 1) & 1]);
+          if (mi > 0) {
+            if (mi < 3)
+              asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+            else
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            asm volatile("" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]));
+          }
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          af[p] = __builtin_bit_cast(
-              bf8, *reinterpret_cast<const u4*>(abase + (((2 * wm + (mi >> 1)) * 2 + (qq >> 1)) * 3 + p) * 1024 +
-                                                16 * 16 * (mi & 1)));
+          for (int ni = 0; ni < 4; ++ni) {
+            if (mi == 0) {
+              // A row 0 and B columns 0..ni landed: younger are 6 (3 - ni) B reads and A row 1's 3
+              if (ni < 2)
+                asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+              else if (ni == 2)
+                asm volatile("s_waitcnt lgkmcnt(9)" ::: "memory");
+              else
+                asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+              if (ni == 0) asm volatile("" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]));
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) mma6_16(af, bf[ni], acc[mi][ni]);
+              for (int p = 0; p < 3; ++p) {
+                asm volatile("" : "+v"(v[ni][p][0]), "+v"(v[ni][p][1]));
+                u4 u;
+                u.x = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][0], v[ni][p][0], 0, 1));
+                u.y = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][0], v[ni][p][0], 2, 3));
+                u.z = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][1], v[ni][p][1], 0, 1));
+                u.w = __builtin_bit_cast(uint32_t, __builtin_shufflevector(v[ni][p][1], v[ni][p][1], 2, 3));
+                bf[ni][p] = __builtin_bit_cast(bf8, u);
+              }
+            }
+            const bf8 af[3] = {__builtin_bit_cast(bf8, cur[0]), __builtin_bit_cast(bf8, cur[1]),
+                               __builtin_bit_cast(bf8, cur[2])};
+            mma6_16(af, bf[ni], acc[mi][ni]);
+            if (mi == 0 || ni == 3) __builtin_amdgcn_sched_barrier(0);  // keep each wait before its MFMAs
+          }
+        }
       }
     }
     // accumulator register r of lane (r16, qq) of tile (mi, ni): row 16 mi + 4 qq + r, column 16 ni + r16
