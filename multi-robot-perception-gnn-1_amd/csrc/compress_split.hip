@@ -884,16 +884,24 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a, int orig, in
   float rsum[G::AJ];
 #pragma unroll
   for (int j = 0; j < G::AJ; ++j) rsum[j] = 0.f;
-  auto load = [&](int s) {
-    const int64_t k = kbeg + (int64_t)s * BK;
-    const int64_t nd = k / a.P, px = k - nd * a.P;
-    const float* gp = a.g + nd * a.gs + px;
-    const float* xp = a.s0 + nd * a.s0s + px;
-    const float* ap = a.s1 + nd * a.s1s + px;
+  // stages in order, k = (node ind, pixel ipx) advanced per stage (P % BK == 0: a stage never straddles
+  // two nodes) — an int64 division per stage put ~80 scalar instructions between the barrier and the
+  // stage's loads
+  int64_t ind = kbeg / a.P;
+  int ipx = (int)(kbeg - ind * a.P);
+  auto load = [&]() {
+    const float* gp = a.g + ind * a.gs + ipx;
+    const float* xp = a.s0 + ind * a.s0s + ipx;
+    const float* ap = a.s1 + ind * a.s1s + ipx;
 #pragma unroll
     for (int j = 0; j < G::AJ; ++j) areg[j] = *reinterpret_cast<const f4*>(gp + aoff[j]);
 #pragma unroll
     for (int j = 0; j < G::BJ; ++j) breg[j] = *reinterpret_cast<const f4*>((bhi[j] ? ap : xp) + boffs[j]);
+    ipx += BK;
+    if (ipx == a.P) {
+      ipx = 0;
+      ++ind;
+    }
   };
   auto store = [&](int buf) {
     char* base = ldsb + buf * G::BUF_BYTES;
@@ -949,7 +957,7 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a, int orig, in
       for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[mi][ni].hi[r] = acc[mi][ni].lo[r] = 0.f;
-    if (nst > 0) load(0);
+    if (nst > 0) load();
 #pragma unroll 1
     for (int s = 0; s < nst; ++s) {
       const int buf = s & 1;
@@ -957,7 +965,7 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a, int orig, in
       store(buf);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (s + 1 < nst) load(s + 1);
+      if (s + 1 < nst) load();
       const char* base = ldsb + buf * G::BUF_BYTES;
       const char* bb = base + 3 * G::A_PART;
       bf8 bf[4][3];
@@ -1000,7 +1008,7 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a, int orig, in
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mi][ni].hi[r] = acc[mi][ni].lo[r] = 0.f;
 
-  if (nst > 0) load(0);
+  if (nst > 0) load();
 #pragma unroll 1
   for (int s = 0; s < nst; ++s) {
     const int buf = s & 1;
@@ -1008,7 +1016,7 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a, int orig, in
     store(buf);  // its buffer was last read in stage s - 2
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (s + 1 < nst) load(s + 1);
+    if (s + 1 < nst) load();
 #pragma unroll
     for (int ksl = 0; ksl < 2; ++ksl) {
       bf8 af[2][3], bf[2][3];
