@@ -4,6 +4,7 @@
 // footprint exceeds 2 x the 256 MB Infinity Cache, one event pair around the replay).
 //   forward mix:  read R, write W (R ~ W)          -> out[i] = in[i]
 //   backward mix: read 2W, write W                  -> out[i] = a[i] + b[i]
+// and each mix in the aggregation kernels' gather pattern (gather_nt, gather2_nt).
 // Kernels: grid-stride float4, nontemporal, 256 threads, one float4 per thread per trip, grid sized
 // to the element count (best of the round-1 copy sweep).  Prints us and the fraction of 8 TB/s.
 // Build: hipcc --offload-arch=gfx950 -O3 tools/copy_ceiling.hip -o tools/bin/copy_ceiling
@@ -58,16 +59,45 @@ __global__ void __launch_bounds__(256) gather_nt(const f4* __restrict__ in, f4* 
   }
 }
 
+// film_bwd_fused's data movement without its Gram, reduction and epilogue: thread = one 16-byte slice;
+// it reads that slice of all NT nodes of grad_out AND of x, and writes NT slices of grad_x (each the
+// sum of the other nodes' grad_out slices plus its own x slice, so every load is used).
 template <int NT>
-static double time_gather(int nsets, int iters, const std::vector<void*>& bufs, size_t n4, size_t node4) {
+__global__ void __launch_bounds__(256) gather2_nt(const f4* __restrict__ g, const f4* __restrict__ x,
+                                                  f4* __restrict__ out, size_t node_stride4, size_t graph_items) {
+  const size_t t = blockIdx.x * (size_t)256 + threadIdx.x;
+  const size_t gi = t / graph_items, r = t - gi * graph_items;
+  const size_t base = gi * NT * node_stride4 + r;
+  f4 v[NT], w[NT];
+#pragma unroll
+  for (int u = 0; u < NT; ++u) v[u] = __builtin_nontemporal_load(g + base + u * node_stride4);
+#pragma unroll
+  for (int u = 0; u < NT; ++u) w[u] = __builtin_nontemporal_load(x + base + u * node_stride4);
+#pragma unroll
+  for (int k = 0; k < NT; ++k) {
+    f4 acc = w[k];
+#pragma unroll
+    for (int u = 0; u < NT; ++u)
+      if (u != k) acc += v[u];
+    __builtin_nontemporal_store(acc, out + base + k * node_stride4);
+  }
+}
+
+template <int NT>
+static double time_gather(int nsets, int iters, const std::vector<void*>& bufs, size_t n4, size_t node4,
+                          bool bwd = false) {
   hipStream_t st;
   CK(hipStreamCreate(&st));
   const size_t graph_items = node4;  // per graph: (channel, slice) items = float4 of one node
   const unsigned grid = (unsigned)((n4 / NT + 255) / 256);
   auto launch = [&](int i) {
     const int s = i % nsets;
-    hipLaunchKernelGGL(gather_nt<NT>, dim3(grid), dim3(256), 0, st, (const f4*)bufs[3 * s], (f4*)bufs[3 * s + 2], node4,
-                       node4);
+    if (bwd)
+      hipLaunchKernelGGL(gather2_nt<NT>, dim3(grid), dim3(256), 0, st, (const f4*)bufs[3 * s],
+                         (const f4*)bufs[3 * s + 1], (f4*)bufs[3 * s + 2], node4, node4);
+    else
+      hipLaunchKernelGGL(gather_nt<NT>, dim3(grid), dim3(256), 0, st, (const f4*)bufs[3 * s], (f4*)bufs[3 * s + 2],
+                         node4, node4);
   };
   (void)graph_items;
   for (int i = 0; i < 2 * nsets; ++i) launch(i);
@@ -170,12 +200,13 @@ int main(int argc, char** argv) {
       const double bytes = (double)plane_bytes * (bwd ? 3 : 2);
       printf("%-10s %s %8.1f MB  %8.2f us  %5.1f %% of 8 TB/s  (%d rotating sets)\n", s.name, bwd ? "2r1w" : "1r1w",
              bytes / 1e6, us, bytes / (us * 1e-6) / 8e12 * 100, nsets);
-      if (!bwd) {  // the forward's gather pattern: N node planes per thread, N outputs
+      {  // the aggregation's gather pattern: N node planes per thread (forward: of x; backward: of
+         // grad_out and x), N outputs
         const size_t node4 = (size_t)s.C * s.HW * s.HW / 4;
-        const double ug = s.N == 8 ? time_gather<8>(nsets, iters, bufs, n4, node4)
-                                   : time_gather<16>(nsets, iters, bufs, n4, node4);
-        printf("%-10s gather%ld %8.1f MB  %8.2f us  %5.1f %% of 8 TB/s\n", s.name, s.N, bytes / 1e6, ug,
-               bytes / (ug * 1e-6) / 8e12 * 100);
+        const double ug = s.N == 8 ? time_gather<8>(nsets, iters, bufs, n4, node4, bwd)
+                                   : time_gather<16>(nsets, iters, bufs, n4, node4, bwd);
+        printf("%-10s %s%ld %8.1f MB  %8.2f us  %5.1f %% of 8 TB/s\n", s.name, bwd ? "gather_bwd" : "gather", s.N,
+               bytes / 1e6, ug, bytes / (ug * 1e-6) / 8e12 * 100);
       }
       fflush(stdout);
       for (auto p : bufs)
