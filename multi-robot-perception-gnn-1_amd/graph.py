@@ -19,6 +19,7 @@ this is checked when the CSR is built (the kernel relies on it).
 from __future__ import annotations
 
 import contextlib
+import warnings
 from typing import Dict, Iterable, List, NamedTuple, Optional, Sequence
 
 import numpy as np
@@ -407,9 +408,9 @@ def save_graphs(filename: str, g_list, labels: Optional[Dict[str, torch.Tensor]]
 
     Format: a NumPy ``.npz`` archive (no pickles) written to ``filename`` as given — the batched
     structure (src, dst, per-graph node/edge counts) plus every node/edge feature and label.  This is
-    this package's own cache format; DGL's binary ``save_graphs`` format is not read (DGL is not
-    available here and the reference ships no cache file to pin it against), so a cache written by
-    DGL must be rebuilt — the reference dataset does that when ``has_cache()`` is False."""
+    this package's own cache format; :func:`load_graphs` reads it and, without DGL, a cache DGL wrote
+    (:mod:`.dgl_format`, parity unpinned).  Writing DGL's format is not offered: with no DGL to check
+    against, a file written here could not be promised to load in DGL."""
     g_list = [g_list] if isinstance(g_list, RobotGraph) else list(g_list)
     arrays = {"magic": np.array(_CACHE_MAGIC), "num_graphs": np.array(len(g_list), np.int64)}
     if g_list:
@@ -426,9 +427,22 @@ def save_graphs(filename: str, g_list, labels: Optional[Dict[str, torch.Tensor]]
         np.savez(f, **arrays)
 
 
+_WARNED_DGL = False
+
+
 def load_graphs(filename: str, idx_list: Optional[Sequence[int]] = None):
     """``dgl.load_graphs`` equivalent: ``(list of graphs, labels dict)`` from :func:`save_graphs`'s
-    format (``dgl/dataloader.py:172-175``); ``idx_list`` selects graphs by index."""
+    format (``dgl/dataloader.py:172-175``); ``idx_list`` selects graphs by index.  A file DGL wrote
+    (``dgl_graph_<N>.bin``, version 2) is read by :mod:`.dgl_format` — parity unpinned (no DGL and
+    no DGL-written file to check it against), said once per process."""
+    from . import dgl_format
+    if dgl_format.is_dgl_graph_file(filename):
+        global _WARNED_DGL
+        if not _WARNED_DGL:
+            _WARNED_DGL = True
+            warnings.warn("mrp_gnn: reading a DGL-written graph file with a reader restated from DGL's "
+                          "serializer and not checked against DGL (parity unpinned)", stacklevel=2)
+        return dgl_format.read_dgl_graphs(filename, idx_list)
     try:
         z = np.load(filename, allow_pickle=False)
     except ValueError as e:

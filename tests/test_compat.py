@@ -9,6 +9,8 @@ import subprocess
 import sys
 import types
 
+import warnings
+
 import numpy as np
 import pytest
 import torch
@@ -215,8 +217,15 @@ def test_graph_cache_round_trip(tmp_path):
     sel, _ = m.load_graphs(path, [2, 0])
     assert [g.num_nodes() for g in sel] == [4, 3]
     assert m.unbatch(m.batch(back))[1].num_edges() == graphs[1].num_edges()
+    # a file with DGL's magic goes to the DGL-format reader (tests/test_dgl_format.py), which
+    # rejects this one (version 0) with a clear error; anything else that is not ours is refused
     foreign = tmp_path / "dgl_written.bin"
     foreign.write_bytes(b"\x3f\xa1\xb4\x46\xf0\x4f\x2e\xdd" + bytes(64))
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        with pytest.raises(ValueError, match="DGL graph file version 0"):
+            m.load_graphs(str(foreign))
+    foreign.write_bytes(b"not a cache at all")
     with pytest.raises(ValueError, match="not an mrp_gnn graph cache"):
         m.load_graphs(str(foreign))
 
