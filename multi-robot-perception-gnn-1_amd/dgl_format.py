@@ -21,7 +21,7 @@ plain containers:
 
 The graph-structure part (the metagraph and the relation graph's sparse matrix, whose inner magic
 numbers and field order this restatement does not rely on) is read structurally: the record's
-named-tensor block is located as the unique offset from which the whole tail parses and ends
+named-tensor block is located as the earliest offset from which the whole tail parses and ends
 exactly at the record's end; the per-type node counts are the vector<i64> just before it; the edge
 list is the relation graph's COO matrix — the last two consecutive integer arrays of one length E
 (E = the edge tensors' leading dimension when there are any) with every value below the node count,
@@ -30,10 +30,12 @@ form whenever the graph has one (``dgl.graph(edge_list)``, as the reference buil
 record holding only CSR/CSC is rejected with a clear error, as are heterographs (more than one
 node or edge type) and file version 1 (DGL < 0.6).  Every check failure raises ``ValueError``.
 
-Host-side file parsing (numpy over one read of the file); no GPU, no torch kernels.
+Host-side file parsing (numpy over a memory map of the file); no GPU, no torch kernels.
 """
 from __future__ import annotations
 
+import mmap
+import os
 import struct
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -110,7 +112,9 @@ class _Reader:
         if min(shape, default=0) < 0 or nbytes != count * bits // 8:
             raise ValueError(f"NDArray at byte {start}: shape {shape} with {nbytes} bytes")
         self.need(nbytes)
-        arr = np.frombuffer(self.buf, dtype=_DTYPES[(code, bits)], count=count, offset=self.pos).reshape(shape)
+        # a writable copy of the bytes: nothing keeps a view into the file's memory map
+        arr = np.frombuffer(bytearray(self.buf[self.pos:self.pos + nbytes]), dtype=_DTYPES[(code, bits)],
+                            count=count).reshape(shape)
         self.pos += nbytes
         return arr, code
 
@@ -133,7 +137,7 @@ class _Reader:
 
 
 def _tensor(arr: np.ndarray, code: int) -> torch.Tensor:
-    t = torch.from_numpy(arr.copy())
+    t = torch.from_numpy(arr)
     return t.view(torch.bfloat16) if code == 4 else t
 
 
@@ -173,15 +177,16 @@ def _locate_tail(buf: bytes, start: int, end: int):
                         cands.append(s)
         p = buf.find(_NDARRAY_MAGIC_BYTES, p + 8, end)
     cands.extend(range(max(start, end - 4096), end))
+    # the earliest offset that parses is the block: a later one is a suffix of it that the last node
+    # tensor's trailing bytes happen to complete (e.g. int64 values 1, 0 read as one node type with
+    # no tensors — seen with random int64 node data)
     found = None
-    for s in cands:
+    for s in sorted(set(cands)):
         try:
-            parsed = _parse_tail(buf, s, end)
+            found = (s, _parse_tail(buf, s, end))
+            break
         except (ValueError, UnicodeDecodeError, struct.error):
             continue
-        if found is not None and found[0] != s:
-            raise ValueError(f"graph record at byte {start}: ambiguous tensor block ({found[0]} and {s})")
-        found = (s, parsed)
     if found is None:
         raise ValueError(f"graph record at byte {start}: no node/edge tensor block ends the record")
     return found
@@ -235,9 +240,17 @@ def read_dgl_graphs(filename: str, idx_list: Optional[Sequence[int]] = None):
     """``dgl.load_graphs(filename, idx_list)`` for a version-2 DGL file: ``(graphs, labels)`` —
     :class:`~mrp_gnn_amd.graph.RobotGraph` objects with their ``ndata``/``edata`` tensors, and the
     label dict.  Parity unpinned (module docstring)."""
-    from .graph import RobotGraph
     with open(filename, "rb") as f:
-        buf = f.read()
+        if os.fstat(f.fileno()).st_size == 0:
+            raise ValueError(f"{filename}: empty file")
+        # memory-mapped: a dataset cache of image frames can be many GB; only the selected graphs'
+        # bytes are touched (tensors are copied out of the map)
+        with mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) as buf:
+            return _read(buf, filename, idx_list)
+
+
+def _read(buf, filename: str, idx_list: Optional[Sequence[int]]):
+    from .graph import RobotGraph
     r = _Reader(buf)
     if r.u64() != FILE_MAGIC:
         raise ValueError(f"{filename}: not a DGL graph file (magic)")

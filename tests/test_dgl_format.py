@@ -100,6 +100,20 @@ def test_isolated_nodes_and_empty_file(tmp_path):
     assert dgl_format.read_dgl_graphs(str(path)) == ([], {})
 
 
+def test_node_data_ending_like_a_tensor_block_header(tmp_path):
+    """int64 node data whose last two values are 1, 0 also parse, from 16 bytes before the edge
+    tensors, as a block with one node type and no node tensors: the earliest parsing offset wins
+    (found with random seg maps in a 100-frame file)."""
+    src, dst, nd, ed = _reference_like(4, 3)
+    seg = nd[2][1].copy()
+    seg.reshape(-1)[-2:] = (1, 0)
+    nd = nd[:2] + [("seg", seg)]
+    path = tmp_path / "g.bin"
+    W.write(path, [W.graph_record(src, dst, 4, nd, ed)] * 2)
+    for g in dgl_format.read_dgl_graphs(str(path))[0]:
+        _check(g, src, dst, nd, ed)
+
+
 def test_csr_only_record_rejected_when_its_arrays_look_like_coo(tmp_path):
     """A CSR-only record whose index arrays happen to fit a COO (E <= N): the indptr before them
     marks it, and it is rejected rather than misread."""
