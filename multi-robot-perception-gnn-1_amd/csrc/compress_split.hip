@@ -758,15 +758,17 @@ constexpr int64_t kOffMax = (int64_t)1 << 31;
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-template <int WMW>
-hipError_t launch_w(Args a, hipStream_t st, const void* fn, void (*kern)(Args)) {
+// one instantiation per kernel, so each kernel's LDS attribute is set (once) for that kernel
+template <int WMW, void (*K)(Args)>
+hipError_t launch_w(Args a, hipStream_t st) {
   using G = Geo<WMW>;
   a.mtiles = (a.M + G::TM - 1) / G::TM;
   const int64_t grid = (int64_t)a.mtiles * ((a.ncols + TN - 1) / TN);
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  static const hipError_t attr = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+  static const hipError_t attr =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(K), hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
+  hipLaunchKernelGGL(K, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
   return hipGetLastError();
 }
 
@@ -802,10 +804,9 @@ hipError_t launch(Args a, hipStream_t st) {
     if (e != hipErrorNotSupported) return e;
   }
   if (v == 7)
-    return launch_w<4>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w4_mf16), gemm_nn_split_w4_mf16);
+    return launch_w<4, gemm_nn_split_w4_mf16>(a, st);
   const bool wide = v == 4 || (v < 0 && a.M % 256 == 0);
-  return wide ? launch_w<4>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w4), gemm_nn_split_w4)
-              : launch_w<2>(a, st, reinterpret_cast<const void*>(&gemm_nn_split_w2), gemm_nn_split_w2);
+  return wide ? launch_w<4, gemm_nn_split_w4>(a, st) : launch_w<2, gemm_nn_split_w2>(a, st);
 }
 
 // ------------------------------------------------------------------------------------------------
