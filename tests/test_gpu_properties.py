@@ -5,6 +5,8 @@ k-NN (regular) graphs, which take the arithmetic-edge-id and per-edge-slot kerne
 backward (dx, dγβ) at the north-star tolerance 1e-5; the forward bit-identical to the oracle wherever
 the reference's reduction is a sequential fp32 sum.  Example counts are bounded (derandomized, no
 example database) so the suite stays a few seconds per property on the GPU box."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -20,7 +22,10 @@ from test_gpu_parity import exact_expected
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-5
-SETTINGS = settings(max_examples=30, deadline=None, derandomize=True, database=None,
+# MRP_PROPERTY_EXAMPLES scales the example count; MRP_PROPERTY_HUNT=1 explores fresh random examples
+# instead of the fixed derandomized set (a bug hunt: hypothesis prints any falsifying example)
+SETTINGS = settings(max_examples=int(os.environ.get("MRP_PROPERTY_EXAMPLES", "30")), deadline=None,
+                    derandomize=not os.environ.get("MRP_PROPERTY_HUNT"), database=None,
                     suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
                                            HealthCheck.function_scoped_fixture])
 MODES = ["film_mean", "film_sum", "copy_mean"]

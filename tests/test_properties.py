@@ -2,6 +2,8 @@
 item 2: arbitrary batches of graphs with up to 16 nodes (``MRP_MAX_NODES``), arbitrary in-degrees
 (zero, multi-edges, self-loops), channels and plane sizes.  The GPU kernels get the same strategies
 against the oracle in tests/test_gpu_properties.py."""
+import os
+
 import numpy as np
 import torch
 from hypothesis import HealthCheck, given, settings
@@ -15,7 +17,10 @@ from graph_strategies import batches
 
 G = importlib.import_module(m.__name__ + ".graph")  # the module (m.graph is the dgl.graph-like constructor)
 
-SETTINGS = settings(max_examples=60, deadline=None, derandomize=True, database=None,
+# MRP_PROPERTY_EXAMPLES scales the example count; MRP_PROPERTY_HUNT=1 explores fresh random examples
+# instead of the fixed derandomized set (a bug hunt: hypothesis prints any falsifying example)
+SETTINGS = settings(max_examples=int(os.environ.get("MRP_PROPERTY_EXAMPLES", "60")), deadline=None,
+                    derandomize=not os.environ.get("MRP_PROPERTY_HUNT"), database=None,
                     suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
 
 
