@@ -4,8 +4,12 @@ Linear (``dgl/model/models.py:146-149``) under ``loss.backward()`` (``dgl/traini
 Every parameter gradient, the logits and the pose gradient are judged against a float64 evaluation
 of the reference layers with the fp32 yardstick (``stack_ref.within``), at the BASELINE shapes
 (E, C) = (1792, 512), (448, 2048), (512, 1024) and small ones; the path taken is asserted."""
+import os
+
 import pytest
 import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
 
 import mrp_gnn_amd as m
 import stack_ref
@@ -101,3 +105,22 @@ def test_split_training_encoder_deterministic_and_repacks(cuda_device):
     assert stack_ref.within(z.detach(), z32, z64)[0]
     for p, a32, a64 in zip(enc.parameters(), g32, g64):
         assert stack_ref.within(p.grad, a32, a64)[0]
+
+
+def _prop_settings():
+    return settings(max_examples=int(os.environ.get("MRP_PROPERTY_EXAMPLES", "12")), deadline=None,
+                    derandomize=not os.environ.get("MRP_PROPERTY_HUNT"), database=None,
+                    suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+
+
+@_prop_settings()
+@given(st.integers(1, 64), st.integers(1, 24), st.sampled_from(["fused", "two_stream", "pose_grad"]))
+def test_split_training_encoder_property(cuda_device, e32, c32, form):
+    """Property form of the test above (hypothesis, bounded and derandomized; ``MRP_PROPERTY_EXAMPLES``
+    / ``MRP_PROPERTY_HUNT`` as in tests/test_gpu_properties.py): any E and C the split training path
+    takes (multiples of 32, E up to 2048, C up to 768) on every backward form."""
+    m.encoder.set_fused_backward(form != "two_stream")
+    try:
+        _check_training_encoder(cuda_device, 32 * e32, 32 * c32, pose_grad=form == "pose_grad")
+    finally:
+        m.encoder.set_fused_backward(True)
