@@ -350,11 +350,11 @@ int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const floa
  *                                      with its own workspace
  *   mrp_edge_encoder_bwd_t             dpre = dh^T (.) [h^T > 0]: dw1 (C, 9) = dpre pose, db1 (C) = row sums
  *                                      (either may be NULL); workspace: _t_workspace(E, C) bytes
- *   mrp_edge_encoder_bwd_fused         the whole backward of the encoder's parameters in four launches on
- *                                      one stream: dz^T; dh^T and dW2 as ONE launch of both split-K
+ *   mrp_edge_encoder_bwd_fused         the whole backward of the encoder's parameters in three launches
+ *                                      on one stream: dz^T; dh^T and dW2 as ONE launch of both split-K
  *                                      products; a reduction that sums their partial tiles, applies the
- *                                      ReLU mask and forms the dW1 / db1 partials (dh^T never written);
- *                                      their final sums.  dw1, db1, dw2, db2 all required (no dpose);
+ *                                      ReLU mask and forms dW1 / db1 (dh^T never written).  dw1, db1,
+ *                                      dw2, db2 all required (no dpose);
  *                                      workspace: _fused_workspace(E, C) bytes
  * Requirements of _bwd_split and _bwd_fused (else hipErrorNotSupported): E % 32 == 0, C % 32 == 0,
  * 16-byte aligned operands.  All sums in a fixed order: deterministic.

@@ -1599,24 +1599,25 @@ extern "C" int mrp_edge_encoder_bwd_split(const float* dz, const float* dzT, con
 }
 
 // ------------------------------------------------------------------------------------------------
-// The edge encoder's whole backward in four launches on one stream (training path, encoder.py):
+// The edge encoder's whole backward in three launches on one stream (training path, encoder.py):
 //   1. dz^T                                     (mrp_edge_encoder_bwd_prep)
 //   2. dh^T = W2^T dz^T and dW2 = dz^T h        one launch of both split-K NT products, splits chosen
 //                                               jointly so the two fill one round of the chip
 //   3. encoder_bwd_reduce: dW2 and db2 = the fixed-order sums of their partial tiles / row sums; and,
-//      per (4 hidden units, 256 edges), dh^T summed from its partial tiles, masked by [h^T > 0]
-//      (ReLU) and reduced against the block's pose rows into dW1 / db1 partials — dh^T never written
-//   4. encoder_bwd_t_final_f: the dW1 / db1 partials summed over the edge blocks in order
+//      per hidden unit (one workgroup over all edges), dh^T summed from its partial tiles, masked by
+//      [h^T > 0] (ReLU) and reduced against the pose rows into dW1 / db1 — dh^T never written.
+//      (Round 4 first reduced per (4 units, 256 edges) into partials summed by a fourth launch: the
+//      whole backward 46.2 -> 42.8 us at E = 1792, C = 512, tools/exp_enc_bwd.py.)
 // ------------------------------------------------------------------------------------------------
 namespace mrp_cs {
 
-constexpr int kNin = 9, kBtE = 256;
+constexpr int kNin = 9;
 
 struct EncPlan {
   int s1, s2;
   int64_t kc1, kc2;
   int t1, t2;  // tiles of each product
-  int64_t off_dzT, off_p1, off_p2, off_p2b, off_t, bytes;
+  int64_t off_dzT, off_p1, off_p2, off_p2b, bytes;
 };
 
 EncPlan enc_plan(int64_t E, int64_t C) {
@@ -1654,52 +1655,49 @@ EncPlan enc_plan(int64_t E, int64_t C) {
   o += al((int64_t)pl.s2 * C2 * C);
   pl.off_p2b = o;
   o += al((int64_t)pl.s2 * C2);
-  pl.off_t = o;
-  o += al(((E + kBtE - 1) / kBtE) * C * (kNin + 1));
   pl.bytes = o * 4;
   return pl;
 }
 
-// blocks [0, nb1): (4 hidden units, 256 edges) of dh^T -> dW1/db1 partials; blocks [nb1, ...): 1024
+// blocks [0, nb1): one hidden unit each -> dW1 / db1; blocks [nb1, ...): 1024
 // outputs of dW2 each (and, in the first 2C / 256 of them, 256 of db2)
 __global__ void __launch_bounds__(256) encoder_bwd_reduce(const float* __restrict__ p1, int s1,
                                                           const float* __restrict__ hT, const float* __restrict__ pose,
-                                                          int E, int C, float* __restrict__ tpart, int nb1,
+                                                          int E, int C, float* __restrict__ dw1,
+                                                          float* __restrict__ db1, int nb1,
                                                           const f4* __restrict__ p2, const float* __restrict__ p2b,
                                                           int s2, f4* __restrict__ dw2, float* __restrict__ db2) {
-  __shared__ float ps[kBtE * kNin];
-  const int neb = (E + kBtE - 1) / kBtE;
   if ((int)blockIdx.x < nb1) {
-    const int ug = blockIdx.x / neb, eb = blockIdx.x - ug * neb, ebase = eb * kBtE;
-    const int nrow = E - ebase < kBtE ? E - ebase : kBtE;
-    for (int i = threadIdx.x; i < nrow * kNin; i += 256) ps[i] = pose[(int64_t)ebase * kNin + i];
-    __syncthreads();
-    const int u = ug * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (u >= C) return;
+    // one workgroup per hidden unit u: wave w's lanes walk edges 64 w + lane + 256 k, summing the dh^T
+    // partials in split order, masking by the ReLU and accumulating d pose^T and d in registers; a
+    // fixed lane butterfly per wave, the four waves' sums added in wave order, and dW1[u] / db1[u]
+    // written directly (no per-edge-block partials, no final launch)
+    __shared__ float wsum[4][kNin + 1];
+    const int u = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t plane = (int64_t)C * E;
+    const float* p1u = p1 + (int64_t)u * E;
+    const float* hTu = hT + (int64_t)u * E;
     float acc[kNin + 1];
 #pragma unroll
     for (int i = 0; i <= kNin; ++i) acc[i] = 0.f;
-#pragma unroll
-    for (int it = 0; it < kBtE / 64; ++it) {
-      const int el = lane + 64 * it;
-      if (el >= nrow) continue;
-      const int64_t o = (int64_t)u * E + ebase + el;
+#pragma unroll 2
+    for (int e = threadIdx.x; e < E; e += 256) {
       float dh;
       if (s1 <= 8) {  // every partial's load issued before the sums (clamped index, no branch per load)
         float pv[8];
 #pragma unroll
-        for (int sp = 0; sp < 8; ++sp) pv[sp] = p1[(int64_t)(sp < s1 ? sp : s1 - 1) * plane + o];
+        for (int sp = 0; sp < 8; ++sp) pv[sp] = p1u[(int64_t)(sp < s1 ? sp : s1 - 1) * plane + e];
         dh = pv[0];
 #pragma unroll
         for (int sp = 1; sp < 8; ++sp) dh = sp < s1 ? dh + pv[sp] : dh;
       } else {
-        dh = p1[o];
-        for (int sp = 1; sp < s1; ++sp) dh += p1[(int64_t)sp * plane + o];
+        dh = p1u[e];
+        for (int sp = 1; sp < s1; ++sp) dh += p1u[(int64_t)sp * plane + e];
       }
-      const float d = hT[o] > 0.f ? dh : 0.f;
+      const float d = hTu[e] > 0.f ? dh : 0.f;
+      const float* pr = pose + (int64_t)e * kNin;
 #pragma unroll
-      for (int i = 0; i < kNin; ++i) acc[i] = fmaf(d, ps[el * kNin + i], acc[i]);
+      for (int i = 0; i < kNin; ++i) acc[i] = fmaf(d, pr[i], acc[i]);
       acc[kNin] += d;
     }
 #pragma unroll
@@ -1710,7 +1708,15 @@ __global__ void __launch_bounds__(256) encoder_bwd_reduce(const float* __restric
       float v = acc[0];
 #pragma unroll
       for (int i = 1; i <= kNin; ++i) v = lane == i ? acc[i] : v;
-      tpart[((int64_t)eb * C + u) * (kNin + 1) + lane] = v;
+      wsum[w][lane] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x <= kNin) {
+      const float v = ((wsum[0][threadIdx.x] + wsum[1][threadIdx.x]) + wsum[2][threadIdx.x]) + wsum[3][threadIdx.x];
+      if (threadIdx.x < kNin)
+        dw1[(int64_t)u * kNin + threadIdx.x] = v;
+      else
+        db1[u] = v;
     }
     return;
   }
@@ -1738,19 +1744,6 @@ __global__ void __launch_bounds__(256) encoder_bwd_reduce(const float* __restric
     for (int sp = 1; sp < s2; ++sp) v += p2b[(int64_t)sp * 2 * C + m];
     db2[m] = v;
   }
-}
-
-__global__ void __launch_bounds__(256) encoder_bwd_t_final_f(const float* __restrict__ part, int neb, int C,
-                                                             float* __restrict__ dw1, float* __restrict__ db1) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= C * (kNin + 1)) return;
-  float s = 0.f;
-  for (int b = 0; b < neb; ++b) s += part[(int64_t)b * C * (kNin + 1) + t];
-  const int k = t / (kNin + 1), i = t - k * (kNin + 1);
-  if (i < kNin)
-    dw1[(int64_t)k * kNin + i] = s;
-  else
-    db1[k] = s;
 }
 
 }  // namespace mrp_cs
@@ -1827,14 +1820,10 @@ extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, con
   hipLaunchKernelGGL(gemm_nt_dual_mf16, dim3((unsigned)(grid1 + grid2)), dim3(GN::THREADS), GN::LDS_BYTES, st, a1,
                      a2, grid1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  const int neb = (int)((E + kBtE - 1) / kBtE);
-  const int nb1 = ((C + 3) / 4) * neb;
+  const int nb1 = C;
   const int64_t nb2 = (C2 * C / 4 + 255) / 256;  // >= 2C / 256 blocks: db2 rides along
   hipLaunchKernelGGL(encoder_bwd_reduce, dim3((unsigned)(nb1 + nb2)), dim3(256), 0, st, ws + pl.off_p1, pl.s1, hT, pose,
-                     num_edges, C, ws + pl.off_t, nb1, reinterpret_cast<const f4*>(ws + pl.off_p2), ws + pl.off_p2b,
+                     num_edges, C, dw1, db1, nb1, reinterpret_cast<const f4*>(ws + pl.off_p2), ws + pl.off_p2b,
                      pl.s2, reinterpret_cast<f4*>(dw2), db2);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(encoder_bwd_t_final_f, dim3((unsigned)((C * (kNin + 1) + 255) / 256)), dim3(256), 0, st,
-                     ws + pl.off_t, neb, C, dw1, db1);
   return hipGetLastError();
 }

@@ -328,7 +328,7 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
 
         if not need[0] and need[1] and need[2] and need[3] and need[4] and _BWD_FUSED:
             # every parameter gradient, no pose gradient (the reference's case: poses are data): the
-            # four-launch single-stream form, dh^T never materialised
+            # three-launch single-stream form, dh^T never materialised
             dw1, db1 = _grad_out(w1, (C, 9), dev), _grad_out(b1, (C,), dev)
             dw2, db2 = _grad_out(w2, (2 * C, C), dev), _grad_out(b2, (2 * C,), dev)
             wsf = torch.empty((int(lib.mrp_edge_encoder_bwd_fused_workspace(E, C)) + 3) // 4, device=dev)

@@ -153,7 +153,7 @@ def test_split_encoder_training_validation_without_launch():
     assert lib.mrp_edge_encoder_bwd_t_workspace(1792, 512) == 7 * 512 * 10 * 4
     assert lib.mrp_edge_encoder_bwd_t(None, 0, None, 0, None, 96, 64, None, None, None, 0, None) == 0  # nothing wanted
     assert lib.mrp_edge_encoder_bwd_t(None, 96, None, 96, None, 96, 64, 16, None, None, 0, None) == HIP_INVALID_VALUE
-    # the fused four-launch backward: all four gradients required, workspace sized by its plan
+    # the fused three-launch backward: all four gradients required, workspace sized by its plan
     ws = lib.mrp_edge_encoder_bwd_fused_workspace(1792, 512)
     assert ws >= (2 * 512 * 1792 + 7 * 512 * 10) * 4  # at least dz^T and the dW1/db1 partials
     assert lib.mrp_edge_encoder_bwd_fused_workspace(100, 512) == 0

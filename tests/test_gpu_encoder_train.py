@@ -28,7 +28,7 @@ def _reference(enc, pose, gz, dtype):
 @pytest.mark.parametrize("form", ["fused", "two_stream", "pose_grad"])
 @pytest.mark.parametrize("E,C", [(1792, 512), (448, 2048), (512, 1024), (96, 64), (32, 32), (224, 160)])
 def test_split_training_encoder_vs_float64(cuda_device, E, C, form):
-    """form: "fused" — parameters only, the four-launch single-stream backward
+    """form: "fused" — parameters only, the three-launch single-stream backward
     (``mrp_edge_encoder_bwd_fused``); "two_stream" — the same with the fused form switched off
     (``_bwd_prep`` / ``_bwd_split`` on two streams / ``_bwd_t``); "pose_grad" — the pose needs a gradient
     too, which only the two-stream form provides."""
