@@ -4,7 +4,9 @@ configs[3] layer shape, the edge encoder at the headline shape) into profiles/<r
 
     python tools/mfma_pmc_summary.py gpurun_out/prof_r04 r04
 
-SQ_VALU_MFMA_BUSY_CYCLES = 32 x the v_mfma_f32_32x32x16_bf16 issued; normalised by 1024 SIMDs x the
+SQ_VALU_MFMA_BUSY_CYCLES = 32 x the v_mfma_f32_32x32x16_bf16 issued, 16 x the v_mfma_f32_16x16x32_bf16
+(the same count for the same products on either shape: 402653184 for both forms of each configs[3]
+GEMM in round 4's passes); normalised by 1024 SIMDs x the
 profiled duration at the 2.4 GHz peak clock, and at the clock the pass ran at (SQ_BUSY_CYCLES over 32
 shader engines x the duration).  The first dispatch of each pass is dropped (cold caches, clock ramp)."""
 import collections
