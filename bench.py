@@ -342,6 +342,8 @@ def train_step_time(gcn, g, x, world, device, args):
         for p in gcn.parameters():
             p.grad = None
         xr.grad = None
+        if reducer is not None:
+            reducer.arm()  # the backward kernels write the gradients straight into the buckets
         gcn(g, xr).backward(grad)
         if reducer is not None:
             reducer.synchronize()
@@ -408,6 +410,8 @@ def config_record(cid, world, rank, device, args):
     def train():
         for p in net.parameters():
             p.grad = None
+        if reducer is not None:
+            reducer.arm()
         net(g, xr).backward(gy)
         if reducer is not None:
             reducer.synchronize()

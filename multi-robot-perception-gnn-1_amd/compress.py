@@ -193,25 +193,31 @@ def compress_backward_data(weight: torch.Tensor, gy: torch.Tensor, gx: torch.Ten
 
 
 def compress_backward_weight(gy: torch.Tensor, x: torch.Tensor, a: torch.Tensor, want_bias: bool = True,
-                             weight: torch.Tensor = None, bias: torch.Tensor = None):
+                             weight: torch.Tensor = None, bias: torch.Tensor = None, want_weight: bool = True):
     """(dW (C, 2C, 1, 1), db (C) or None) = (sum_n gy[n] [x[n]; a[n]]^T, sum gy)
     (``mrp_compress_bwd_weight``); None when the kernel declines the shape (H W % 32 != 0).  Given
     the parameters, the results are written straight into a gradient all-reducer's buckets when
-    one holds them (``dist.grad_out_like``)."""
+    one holds them (``dist.grad_out_like``) — only for a gradient that is wanted, and the slots are
+    given back (``dist.release_grad_out``) when the kernel declines the shape."""
     from .aggregate import _ptr, _stream
-    from .dist import grad_out_like
+    from .dist import grad_out_like, release_grad_out
     n, C, H, W = gy.shape
     lib = _lib.load_library()
     gy, gs = _node_major(gy)
     x, xs = _node_major(x)
     a, as_ = _node_major(a)
-    dw = grad_out_like(weight) if weight is not None and weight.dim() == 4 else None
-    if dw is None:
+    claimed = []
+    dw = grad_out_like(weight) if want_weight and weight is not None and weight.dim() == 4 else None
+    if dw is not None:
+        claimed.append((weight, dw))
+    else:
         dw = torch.empty((C, 2 * C, 1, 1), device=gy.device, dtype=torch.float32)
     db = None
     if want_bias:
         db = grad_out_like(bias) if bias is not None else None
-        if db is None:
+        if db is not None:
+            claimed.append((bias, db))
+        else:
             db = torch.empty((C,), device=gy.device, dtype=torch.float32)
     P = H * W
     split = _split("wgrad") and C % 64 == 0 and P % 32 == 0
@@ -226,6 +232,8 @@ def compress_backward_weight(gy: torch.Tensor, x: torch.Tensor, a: torch.Tensor,
         code = fn(_ptr(gy), gs, _ptr(x), xs, _ptr(a), as_, n, C, P, _ptr(dw), _ptr(db), _ptr(ws), nbytes,
                   _stream(gy.device))
     if code == _lib.HIP_ERROR_NOT_SUPPORTED:
+        for p, v in claimed:
+            release_grad_out(p, v)
         return None
     _lib.check(code, name)
     return dw, db
@@ -363,7 +371,8 @@ class FilmCompressFunction(torch.autograd.Function):
             if dgb is not None:
                 dgb = dgb.view(gb.shape).to(gb.dtype)
         if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
-            r = compress_backward_weight(gy, x, agg, ctx.has_bias, weight, bias) if ctx.hip else None
+            r = compress_backward_weight(gy, x, agg, ctx.has_bias and ctx.needs_input_grad[3], weight, bias,
+                                         want_weight=ctx.needs_input_grad[2]) if ctx.hip else None
             dw, db = r if r is not None else _lib_backward_weight(gy, x, agg, ctx.has_bias)
             if not ctx.needs_input_grad[2]:
                 dw = None

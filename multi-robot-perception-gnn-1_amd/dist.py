@@ -87,17 +87,30 @@ _ACTIVE = weakref.WeakSet()
 
 
 def grad_out_like(param: torch.Tensor) -> Optional[torch.Tensor]:
-    """Where a backward kernel should write ``param``'s gradient: a fresh view of the slot a live
-    :class:`GradAllReducer` keeps for it in its flat bucket, or None (allocate normally).  Autograd's
-    AccumulateGrad then adopts the returned tensor as ``param.grad`` without a copy (a freshly made,
-    unshared tensor with the parameter's layout), so the gradient is already in the all-reduce
-    buffer.  Handed out once per step and only while ``param.grad`` is None (a gradient that
-    accumulates onto an existing one is written elsewhere and added by autograd as usual)."""
+    """Where a backward kernel should write ``param``'s gradient: a fresh view of the slot a live,
+    ARMED :class:`GradAllReducer` keeps for it in its flat bucket, or None (allocate normally).
+    Autograd's AccumulateGrad then adopts the returned tensor as ``param.grad`` without a copy (a
+    freshly made, unshared tensor with the parameter's layout), so the gradient is already in the
+    all-reduce buffer.  Handed out once per step, only while ``param.grad`` is None (a gradient that
+    accumulates onto an existing one is written elsewhere and added by autograd as usual), only for
+    fp32 parameters (the HIP kernels write fp32), and only between :meth:`GradAllReducer.arm` (or
+    ``set_local_count``) and ``synchronize()`` — a backward the reducer is not meant to see (e.g.
+    ``torch.autograd.grad``) gets ordinary tensors.  A caller whose kernel then declines the shape
+    gives the slot back with :func:`release_grad_out`."""
     for red in list(_ACTIVE):
         v = red.claim(param)
         if v is not None:
             return v
     return None
+
+
+def release_grad_out(param: Optional[torch.Tensor], view: Optional[torch.Tensor]) -> None:
+    """Undo :func:`grad_out_like` for a slot that was not written (the kernel declined the shape):
+    the gradient computed elsewhere then takes the hook's copy path as usual."""
+    if param is None or view is None:
+        return
+    for red in list(_ACTIVE):
+        red.release(param, view)
 
 
 class GradAllReducer:
@@ -108,7 +121,16 @@ class GradAllReducer:
     with no per-step concatenation and no copy back.  A gradient that autograd allocated on its
     own (``zero_grad(set_to_none=True)`` and an op that did not write through :func:`grad_out_like`)
     is copied into its slot once, in the hook; with ``set_to_none=False`` autograd accumulates
-    straight into the views.  ``copies`` counts those hook copies (tests)."""
+    straight into the views.  ``copies`` counts those hook copies (tests).
+
+    Slots start at multiples of :attr:`SLOT_ALIGN` bytes (the HIP kernels that write gradients in
+    place take 16-byte aligned pointers; parameters of any size may precede them in a bucket).
+    Kernels are handed slots only while the reducer is armed (:meth:`arm`, or ``set_local_count``),
+    until ``synchronize()``; arming re-keys the slot lookup on the parameters' current storage, so
+    a model moved in place after the reducer was built keeps the zero-copy path, and a parameter
+    that changed device or dtype raises (its bucket lives on the old device / dtype)."""
+
+    SLOT_ALIGN = 256
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 32 << 20,
                  group: Optional[dist.ProcessGroup] = None):
@@ -131,12 +153,16 @@ class GradAllReducer:
         self._flat: List[torch.Tensor] = []
         for bi, b in enumerate(self.buckets):
             off = 0
+            align = max(1, self.SLOT_ALIGN // b[0].element_size())
             for p in b:
+                off = -(-off // align) * align  # every slot starts SLOT_ALIGN-byte aligned
                 self._slot[id(p)] = (bi, off, p.numel())
-                self._by_ptr[(p.data_ptr(), p.device)] = p
                 off += p.numel()
-            self._flat.append(torch.zeros(off, dtype=b[0].dtype, device=b[0].device))
+            self._flat.append(torch.zeros(max(off, 1), dtype=b[0].dtype, device=b[0].device))
+        self._params = [p for b in self.buckets for p in b]
         self._bucket_of = {k: v[0] for k, v in self._slot.items()}
+        self._armed = False
+        self._rekey()
         self._scale = 1.0 / self.world
         self._empty = False  # this rank holds no graphs this step (set_local_count(0))
         self.copies = 0
@@ -162,7 +188,27 @@ class GradAllReducer:
         # an empty shard (more ranks than graphs, e.g. a DataLoader's short last batch) has a mean loss
         # of 0/0 = NaN: its contribution must be exact zeros, since 0 * NaN would poison every rank
         self._empty = n_local == 0
+        self.arm()
         return self._scale
+
+    def arm(self) -> "GradAllReducer":
+        """Hand bucket slots to the backward kernels (:func:`grad_out_like`) until ``synchronize()``.
+        Re-keys the lookup on the parameters' current storage; raises if a parameter moved to another
+        device or dtype after the reducer was built.  Returns self (``reducer.arm(); loss.backward()``)."""
+        self._rekey()
+        self._armed = True
+        return self
+
+    def _rekey(self) -> None:
+        by_ptr = {}
+        for p in self._params:
+            flat = self._flat[self._bucket_of[id(p)]]
+            if p.device != flat.device or p.dtype != flat.dtype:
+                raise RuntimeError(f"GradAllReducer: a parameter is now {p.dtype} on {p.device} but its bucket is "
+                                   f"{flat.dtype} on {flat.device} (moved or re-cast after the reducer was built); "
+                                   "build a new GradAllReducer")
+            by_ptr[(p.data_ptr(), p.device)] = p
+        self._by_ptr = by_ptr
 
     def _device(self):
         for b in self.buckets:
@@ -176,12 +222,21 @@ class GradAllReducer:
 
     def claim(self, t: torch.Tensor) -> Optional[torch.Tensor]:
         """:func:`grad_out_like` for this reducer's parameters (see there)."""
+        if not self._armed:
+            return None
         p = self._by_ptr.get((t.data_ptr(), t.device))
-        if p is None or p.shape != t.shape or p.grad is not None or id(p) in self._handed \
+        if p is None or p.shape != t.shape or p.dtype != torch.float32 or t.dtype != torch.float32 \
+                or not p.is_contiguous() or p.grad is not None or id(p) in self._handed \
                 or self._work[self._bucket_of[id(p)]] is not None:
             return None
         self._handed.add(id(p))
         return self.view(p)
+
+    def release(self, t: torch.Tensor, view: torch.Tensor) -> None:
+        """:func:`release_grad_out`: give back a slot handed out for ``t`` (matched by the view)."""
+        p = self._by_ptr.get((t.data_ptr(), t.device))
+        if p is not None and id(p) in self._handed and view.data_ptr() == self.view(p).data_ptr():
+            self._handed.discard(id(p))
 
     def reset(self) -> None:
         self.events = []
@@ -238,6 +293,7 @@ class GradAllReducer:
             self._work[bi].wait()
         self.last_events = self.events
         self.reset()
+        self._armed = False
 
     def remove(self) -> None:
         for h in self._hooks:

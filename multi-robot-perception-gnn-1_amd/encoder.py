@@ -105,7 +105,7 @@ def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
     if not pose.is_cuda:
         raise RuntimeError("mrp_gnn: the edge encoder kernel runs only on the GPU; no CPU fallback")
     if C % 32 != 0 or tuple(l1.weight.shape) != (C, 9) or tuple(l2.weight.shape) != (2 * C, C) \
-            or l1.bias is None:
+            or l1.bias is None or not image_supported(C):
         return None
     img = packed_weights(l1, l2)
     pose = pose.detach().contiguous().float()
@@ -281,10 +281,19 @@ def transposed_w2(l2: torch.nn.Linear) -> torch.Tensor:
     return t
 
 
+def image_supported(C: int) -> bool:
+    """The packed split-bf16 weight image exists for C: C % 32 == 0 and the image under 2^31 bytes
+    (``mrp_edge_encoder_pack`` declines C > 13344)."""
+    return C > 0 and C % 32 == 0 and 0 < int(_lib.load_library().mrp_edge_encoder_pack_bytes(C)) < (1 << 31)
+
+
 def split_train_supported(E: int, C: int) -> bool:
     """The split-bf16 training path's shapes: C % 32 == 0 and E % 32 == 0 (its backward GEMMs walk
-    the edges in 32-edge stages); the reference configurations all qualify (E = B N (N - 1) or B N k)."""
-    return E > 0 and C > 0 and C % 32 == 0 and E % 32 == 0
+    the edges in 32-edge stages), the weight image under 2^31 bytes and every operand (z, dz^T, h^T:
+    E x 2C floats at most) addressable with 32-bit offsets; the reference configurations all qualify
+    (E = B N (N - 1) or B N k).  Other shapes train through :class:`EdgeEncoderFunction`."""
+    return (E > 0 and C > 0 and C % 32 == 0 and E % 32 == 0 and E * 2 * C * 4 < (1 << 31)
+            and image_supported(C))
 
 
 class EdgeEncoderSplitFunction(torch.autograd.Function):

@@ -322,6 +322,7 @@ def _views_worker(rank, world, port):
             else:
                 for p in params:
                     p.grad.zero_()  # zero_grad(set_to_none=False): accumulate into the views
+            red.arm()  # slots are handed to the kernels only for the backward the reducer reduces
             torch.nn.functional.mse_loss(_MatW.apply(lin(data[lo:hi]), w), target[lo:hi]).backward()
             red.synchronize()
             copies = red.copies - before
@@ -340,6 +341,59 @@ def _views_worker(rank, world, port):
 
 def test_grad_allreduce_bucket_views_world2():
     mp.spawn(_views_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _slot_rules_worker(rank, world, port):
+    """every slot is SLOT_ALIGN-byte aligned whatever precedes it in the bucket; slots go
+    to kernels only while armed; non-fp32 parameters never get one; a slot a kernel declined is given
+    back; arming re-keys on moved storage and raises on a device / dtype change."""
+    from mrp_gnn_amd.dist import grad_out_like, release_grad_out
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # odd numels first in backward order (registration order reversed): the decoder-before-encoder
+        # layout of multi_view_dgl_model, whose last conv bias has num_classes + 1 elements
+        enc = torch.nn.Parameter(torch.randn(64, 9))
+        odd = [torch.nn.Parameter(torch.randn(n)) for n in (3, 5, 7)]
+        half = torch.nn.Parameter(torch.randn(8).half())
+        params = [enc] + odd
+        red = GradAllReducer(params + [half], bucket_bytes=1 << 20)
+        for p in params:  # relative to the bucket's base (torch's GPU allocator aligns it to >= 512 B)
+            base = red._flat[red._bucket_of[id(p)]].data_ptr()
+            assert (red.view(p).data_ptr() - base) % GradAllReducer.SLOT_ALIGN == 0
+        assert grad_out_like(enc) is None  # not armed
+        red.arm()
+        assert grad_out_like(half) is None  # fp16: the HIP kernels write fp32
+        v = grad_out_like(enc)
+        assert v is not None and v.data_ptr() == red.view(enc).data_ptr()
+        assert grad_out_like(enc) is None  # once per step
+        release_grad_out(enc, v)  # the kernel declined: the slot is free again
+        v2 = grad_out_like(enc)
+        assert v2 is not None and v2.data_ptr() == v.data_ptr()
+        loss = (enc.sum() + sum(p.sum() for p in odd) + half.float().sum()) * (rank + 1)
+        loss.backward()
+        red.synchronize()
+        assert grad_out_like(odd[0]) is None  # disarmed by synchronize()
+        for p in params:
+            assert torch.allclose(p.grad, torch.full_like(p, 1.5))
+        # storage moved in place (e.g. model.to() onto the same device re-allocating): re-keyed on arm
+        enc.data = enc.data.clone()
+        for p in params + [half]:
+            p.grad = None
+        red.arm()
+        assert grad_out_like(enc) is not None
+        red.synchronize()
+        enc.data = enc.data.double()
+        with pytest.raises(RuntimeError, match="re-cast"):
+            red.arm()
+        red.remove()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_slot_rules_world2():
+    mp.spawn(_slot_rules_worker, args=(2, _free_port()), nprocs=2, join=True)
 
 
 def test_bench_self_launch_command():

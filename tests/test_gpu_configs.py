@@ -9,7 +9,7 @@ is accepted when its error against the float64 stack is within max(1e-5, 4 x the
 restatement computed in fp32) — the HIP path is as accurate as an fp32 run of the reference's ops.
 
 Configs (BASELINE.json ``configs``):
-  [1] B=16, N=8 complete, C=512, 32x32, 2 layers (multi_gcn + compress)   -- covered at B=4 here
+  [1] B=16, N=8 complete, C=512, 32x32, 2 layers (multi_gcn + compress)
   [2] B=32, N=8 complete, C=1280, 8x8, gcn1 -> cat -> conv1 (gcn_compress)
   [3] B=8 per GPU (32 over 4), N=8 complete, C=2048, 8x8, 2 layers (multi_gcn + compress)
   [4] B=8 per GPU (64 over 8), N=16 k-NN(4), C=1024, 16x16, 3 layers
@@ -84,6 +84,13 @@ def test_config4_full_size(cuda_device):
     """configs[4]: 16-robot k-NN(4), C=1024, 16x16, 8 graphs per GPU, 3 GCN layers (the k-NN frames are
     MRP_GRAPH_REGULAR(4): per-edge-slot forward and backward)."""
     check_config(cuda_device, B=8, N=16, C=1024, H=16, layers=3, knn=4)
+
+
+def test_config1_full_size(cuda_device):
+    """configs[1]: 8-robot warehouse, ResNet18 C=512 at H/8 x W/8 = 32x32, batch 16, 2 layers (multi_gcn +
+    compress, ``dgl/model/models.py:180-189``) — the grid sizes the benchmark runs (forward, dx and
+    every parameter gradient against float64)."""
+    check_config(cuda_device, B=16, N=8, C=512, H=32, layers=2)
 
 
 def test_config1_shape_reduced_batch(cuda_device):
