@@ -830,6 +830,7 @@ struct NTArgs {
   float* outb;  // [split][M] or null
   int64_t ktot, kchunk;
   int32_t M, N, n0, P, mtiles, ntiles;
+  const u4* ap;  // gemm_nt_psa: the pre-split image of g (split_rows), KS = ktot / 16 16-k steps per row block
 };
 
 template <int WMW>
@@ -1062,6 +1063,269 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_split_w4(NTArgs a) {
 __global__ void __launch_bounds__(512, 1) gemm_nt_split_w4_mf16(NTArgs a) {
   gemm_nt_split_body<4, true>(a, blockIdx.x, gridDim.x);
 }
+
+// ------------------------------------------------------------------------------------------------
+// Weight gradient with a pre-split A (round 5; split_nt 4, the default where C >= 1024).  The kernel
+// above splits BOTH operands in every workgroup: A = dy (M = C rows) is re-split by every column tile
+// (2C / 128 of them: 32 at configs[3]) and B = [x; agg] by every row tile (C / 256), three times the
+// NN kernel's split work per MFMA (PMC r04: 1.59x its VALU instructions, MFMA busy 0.55 vs 0.66).
+// Here dy is split ONCE, by split_rows, into `pack`'s fragment-ordered image (4 bytes read and 6
+// written per element, plus the row sums db in fixed-order groups), and arrives by LDS-DMA exactly as
+// the NN kernel's weight does; B is split in-kernel as before.  Per output the products and their
+// order are gemm_nt_split_body<4, true>'s, so at the same split dW is bit-identical to it.
+// ------------------------------------------------------------------------------------------------
+
+// g (nodes, M, P), node stride gs -> the packed A image of the M x K matrix, k = node P + pixel
+// (P % 16 == 0): unit ((mb KS + ks) 3 + p) 64 + lane holds lane (r = lane & 31, h = lane >> 5)'s
+// k = 16 ks + 8 h .. + 7 of row 32 mb + r, part p — `pack`'s layout.  One wave per (row block mb,
+// group of G 16-k steps); its row sums over the group go to rsum[m][group] (null: none), the two lanes
+// of a row added in one fixed order.
+__global__ void __launch_bounds__(256) split_rows(const float* __restrict__ g, int64_t gs, int32_t M, int32_t P,
+                                                  int64_t KS, int32_t G, int32_t ngroups, u4* __restrict__ out,
+                                                  float* __restrict__ rsum) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wv = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int MB = M / 32;
+  if (wv >= (int64_t)MB * ngroups) return;
+  const int mb = (int)(wv % MB), grp = (int)(wv / MB);
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t ks0 = (int64_t)grp * G;
+  const int64_t ks1 = ks0 + G < KS ? ks0 + G : KS;
+  int64_t nd = 16 * ks0 / P;  // the step's node and first pixel (P % 16 == 0: a step is within a node)
+  int px = (int)(16 * ks0 - nd * P);
+  const float* row = g + (int64_t)(32 * mb + r) * P + 8 * h;
+  u4* o = out + ((int64_t)mb * KS * 3) * 64 + lane;
+  float sum = 0.f;
+#pragma unroll 2
+  for (int64_t ks = ks0; ks < ks1; ++ks) {
+    const float* src = row + nd * gs + px;
+    const f4 v0 = *reinterpret_cast<const f4*>(src), v1 = *reinterpret_cast<const f4*>(src + 4);
+    sum += ((v0.x + v0.y) + (v0.z + v0.w)) + ((v1.x + v1.y) + (v1.z + v1.w));
+    u4 p0, p1, p2;
+    const f2 x[4] = {{v0.x, v0.y}, {v0.z, v0.w}, {v1.x, v1.y}, {v1.z, v1.w}};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t e0, e1, e2;
+      split2(x[i], e0, e1, e2);
+      p0[i] = e0, p1[i] = e1, p2[i] = e2;
+    }
+    u4* d = o + ks * 3 * 64;
+    __builtin_nontemporal_store(p0, d);
+    __builtin_nontemporal_store(p1, d + 64);
+    __builtin_nontemporal_store(p2, d + 128);
+    px += 16;
+    if (px == P) {
+      px = 0;
+      ++nd;
+    }
+  }
+  if (rsum != nullptr) {
+    const float other = __shfl_xor(sum, 32, 64);
+    const float tot = h == 0 ? sum + other : other + sum;
+    if (h == 0) rsum[(int64_t)(32 * mb + r) * ngroups + grp] = tot;  // [m][group]: a row's partials contiguous
+  }
+}
+
+// out[m] = the sum of part[m][0 .. n) in a fixed order: one wave per row, lane l adding partials
+// l, l + 64, .. in order, then a fixed xor butterfly (every lane ends with the same value)
+__global__ void __launch_bounds__(64) row_sums(const float* __restrict__ part, int32_t n, int32_t M,
+                                               float* __restrict__ out) {
+  const int m = blockIdx.x, lane = threadIdx.x;
+  if (m >= M) return;
+  const float* p = part + (int64_t)m * n;
+  float v = 0.f;
+  for (int i = lane; i < n; i += 64) v += p[i];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane == 0) out[m] = v;
+}
+
+__device__ __forceinline__ void gemm_nt_psa_body(const NTArgs& a, int orig, int nwg) {
+  using G = NTGeo<4>;
+  constexpr int A_BYTES = 48 * 1024;  // 256 rows x 32 k x 3 parts: 48 1-KiB pieces, 6 per wave
+  constexpr int BP = G::B_PART, BUF = A_BYTES + 3 * BP;  // 72 KiB per buffer, two buffers
+  extern __shared__ u4 lds[];
+  char* ldsb = reinterpret_cast<char*>(lds);
+  const int q8 = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + orig / 8;
+  const int tiles = a.mtiles * a.ntiles;
+  const int split = id / tiles, tid = id - split * tiles;
+  const int mt = tid % a.mtiles, nt = tid / a.mtiles;
+  const int mbase = mt * G::TM, nbase = nt * TN;
+  const int64_t kbeg = (int64_t)split * a.kchunk;
+  const int64_t kend = kbeg + a.kchunk < a.ktot ? kbeg + a.kchunk : a.ktot;
+  const int nst = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int64_t KS = a.ktot / 16;
+  const int MB = a.M / 32;
+
+  // ---- A: LDS-DMA pieces pc = (mbl 2 + ksl) 3 + p of the stage, pc = w + 8 i
+  const __amdgpu_buffer_rsrc_t ra = rsrc(a.ap);
+  uint32_t va[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int pc = w + 8 * i;
+    const int mbl = pc / 6, kp = pc % 6;
+    const int mb = min(mt * 8 + mbl, MB - 1);  // blocks past M: any valid data, never stored
+    va[i] = (uint32_t)((((int64_t)mb * KS + kbeg / 16) * 3 + kp) * 64 + lane) * 16;
+  }
+  auto issue_a = [&](int s, int buf) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, lds + (buf * BUF + (w + 8 * i) * 1024) / 16, 16, va[i],
+                                               (uint32_t)s * 6 * 1024, 0, 0);
+  };
+
+  // ---- B: thread t -> piece (t & 7) (4 pixels) of rows (t >> 3) + 64 j of the stage
+  const int pc4 = threadIdx.x & 7, r0 = threadIdx.x >> 3;
+  int64_t boffs[G::BJ];
+  bool bhi[G::BJ];
+#pragma unroll
+  for (int j = 0; j < G::BJ; ++j) {
+    const int n = min(nbase + r0 + G::RPP * j, a.N - 1);
+    bhi[j] = n >= a.n0;
+    boffs[j] = (int64_t)(bhi[j] ? n - a.n0 : n) * a.P + 4 * pc4;
+  }
+  f4 breg[G::BJ];
+  int64_t ind = kbeg / a.P;
+  int ipx = (int)(kbeg - ind * a.P);
+  auto load_b = [&]() {
+    const float* xp = a.s0 + ind * a.s0s + ipx;
+    const float* ap = a.s1 + ind * a.s1s + ipx;
+#pragma unroll
+    for (int j = 0; j < G::BJ; ++j) breg[j] = *reinterpret_cast<const f4*>((bhi[j] ? ap : xp) + boffs[j]);
+    ipx += BK;
+    if (ipx == a.P) {
+      ipx = 0;
+      ++ind;
+    }
+  };
+  auto store_b = [&](int buf) {
+    char* img = ldsb + buf * BUF + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < G::BJ; ++j) {
+      u2 p0, p1, p2;
+      f2 lo, hi;
+      lo.x = breg[j].x, lo.y = breg[j].y, hi.x = breg[j].z, hi.y = breg[j].w;
+      uint32_t l0, l1, l2, h0, h1, h2;
+      split2(lo, l0, l1, l2);
+      split2(hi, h0, h1, h2);
+      p0.x = l0, p1.x = l1, p2.x = l2, p0.y = h0, p1.y = h1, p2.y = h2;
+      const uint32_t o = rowoff(r0 + G::RPP * j, pc4 >> 1) + 8 * (pc4 & 1);
+      *reinterpret_cast<u2*>(img + o) = p0;
+      *reinterpret_cast<u2*>(img + BP + o) = p1;
+      *reinterpret_cast<u2*>(img + 2 * BP + o) = p2;
+    }
+  };
+
+  // fragments: lane (r16, qq) holds k = 8 qq .. 8 qq + 7 of row r16 of a 16-row block.  A: 16-row block mi
+  // of the wave is half (mi & 1) of 32-row block 2 wm + (mi >> 1); the packed image holds 16-k steps in the
+  // 32 x 32 x 16 lane order, so the lane reads step qq >> 1, slot 16 (mi & 1) + r16 + 32 (qq & 1) (the NN
+  // kernel's A reads).  B: chunk qq of row 64 wn + 16 ni + r16 of the [row][32 k] images.
+  const int r16 = lane & 15, qq = lane >> 4;
+  const uint32_t abase0 = (uint32_t)reinterpret_cast<uintptr_t>(ldsb + (r16 + 32 * (qq & 1)) * 16 +
+                                                                 ((4 * wm + (qq >> 1)) * 3) * 1024);
+  uint32_t bro[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni)
+    bro[ni] = (uint32_t)reinterpret_cast<uintptr_t>(ldsb + A_BYTES + rowoff(64 * wn + 16 * ni + r16, qq));
+  Acc2s acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mi][ni].hi[r] = acc[mi][ni].lo[r] = 0.f;
+  if (nst > 0) {
+    issue_a(0, 0);
+    load_b();
+  }
+#pragma unroll 1
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage s's B registers and own A pieces landed
+    store_b(buf);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage s complete for every wave; every wave is past stage s - 1's reads
+    {
+      // every fragment read by inline asm with counted waits (a C++ LDS read beside the LDS-DMA issued
+      // below would make hipcc wait for the DMA): A row 0, B columns 0..3, then A row mi + 1 under row
+      // mi's MFMAs
+      const uint32_t ab = abase0 + (uint32_t)(buf * BUF);
+      u4 ar[2][3], br[4][3];
+      auto read_a16 = [&](int mi, u4 (&rg)[3]) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          asm volatile("ds_read_b128 %0, %1 offset:%2"
+                       : "=v"(rg[p])
+                       : "v"(ab), "i"((mi >> 1) * 6144 + p * 1024 + 256 * (mi & 1)));
+      };
+      read_a16(0, ar[0]);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          asm volatile("ds_read_b128 %0, %1 offset:%2"
+                       : "=v"(br[ni][p])
+                       : "v"(bro[ni] + (uint32_t)(buf * BUF)), "i"(p * BP));
+      if (s + 1 < nst) {
+        issue_a(s + 1, buf ^ 1);
+        load_b();
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        u4 (&cur)[3] = ar[mi & 1];
+        if (mi < 3) read_a16(mi + 1, ar[(mi + 1) & 1]);
+        if (mi > 0) {
+          if (mi < 3)
+            asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+          else
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          asm volatile("" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]));
+        }
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          if (mi == 0) {
+            // A row 0 and B columns 0..ni landed: younger are 3 (3 - ni) B reads and A row 1's 3
+            if (ni == 0)
+              asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+            else if (ni == 1)
+              asm volatile("s_waitcnt lgkmcnt(9)" ::: "memory");
+            else if (ni == 2)
+              asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+            else
+              asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+            if (ni == 0) asm volatile("" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]));
+            asm volatile("" : "+v"(br[ni][0]), "+v"(br[ni][1]), "+v"(br[ni][2]));
+          }
+          const bf8 af[3] = {__builtin_bit_cast(bf8, cur[0]), __builtin_bit_cast(bf8, cur[1]),
+                             __builtin_bit_cast(bf8, cur[2])};
+          const bf8 bfr[3] = {__builtin_bit_cast(bf8, br[ni][0]), __builtin_bit_cast(bf8, br[ni][1]),
+                              __builtin_bit_cast(bf8, br[ni][2])};
+          mma6_16(af, bfr, acc[mi][ni]);
+          if (mi == 0 || ni == 3) __builtin_amdgcn_sched_barrier(0);  // keep each wait before its MFMAs
+        }
+      }
+    }
+  }
+  float* out = a.out + (int64_t)split * a.M * a.N;
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int n = nbase + 64 * wn + 16 * ni + r16;
+    if (n >= a.N) continue;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mbase + 64 * wm + 16 * mi + 4 * qq + r;
+        if (m < a.M) out[(int64_t)m * a.N + n] = __fadd_rn(acc[mi][ni].hi[r], acc[mi][ni].lo[r]);
+      }
+  }
+}
+
+__global__ void __launch_bounds__(512, 1) gemm_nt_psa(NTArgs a) { gemm_nt_psa_body(a, blockIdx.x, gridDim.x); }
 
 // Pipelined weight-gradient form (round 4; the default where its layout conditions hold).  The NN
 // kernel's schedule (gemm_nn_split3_body) for two activation operands: 256 x 128 tiles of 8 waves of
@@ -1317,10 +1581,10 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_dual_mf16(NTArgs a1, NTArgs a2
     gemm_nt_split_body<4, true>(a2, blockIdx.x - grid1, gridDim.x - grid1);
 }
 
-// out = sum over the splits of part (fixed order), the same for the row sums
+// out = sum over the splits of part (fixed order); outb = the same over nsplitb row-sum partials
 __global__ void __launch_bounds__(256) split_sum_nt(const f4* __restrict__ part, int nsplit, int64_t n4,
-                                                    f4* __restrict__ out, const float* __restrict__ partb, int32_t M,
-                                                    float* __restrict__ outb) {
+                                                    f4* __restrict__ out, const float* __restrict__ partb,
+                                                    int nsplitb, int32_t M, float* __restrict__ outb) {
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t e = tid; e < n4; e += stride) {
@@ -1331,7 +1595,7 @@ __global__ void __launch_bounds__(256) split_sum_nt(const f4* __restrict__ part,
   if (outb != nullptr)
     for (int64_t m = tid; m < M; m += stride) {
       float v = partb[m];
-      for (int s = 1; s < nsplit; ++s) v += partb[(int64_t)s * M + m];
+      for (int s = 1; s < nsplitb; ++s) v += partb[(int64_t)s * M + m];
       outb[m] = v;
     }
 }
@@ -1471,11 +1735,12 @@ hipError_t nt_run(NTArgs a, int64_t M, int64_t N, int32_t nodes, float* out, flo
   a.N = (int32_t)N;
   const int64_t grid = (int64_t)a.mtiles * a.ntiles * ns;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  // split_nt: -1 / 3 (default) the 32-k-stage form on 16x16x32 MFMAs — 4-5 % faster than either
+  // split_nt (the compress weight gradient takes nt_run_psa first at 4, and at -1 where C >= 1024):
+  // -1 / 3 the 32-k-stage form on 16x16x32 MFMAs — 4-5 % faster than either
   // 32x32x16 form at every config shape (tools/exp_nt_forms.py: the chip holds a higher clock for that
   // shape under its power limit); 2 the pipelined 16-k-stage 32x32x16 form; 1 the 32-k-stage one
   const int v = mrp_host::tuning().split_nt;
-  if (v == 3 || v < 0) {
+  if (v == 3 || v == 4 || v < 0) {
     static const hipError_t attr16 = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split_w4_mf16),
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
     if (attr16 != hipSuccess) return attr16;
@@ -1485,7 +1750,7 @@ hipError_t nt_run(NTArgs a, int64_t M, int64_t N, int32_t nodes, float* out, flo
     const int64_t n4 = M * N / 4;
     const int64_t blocks = (n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048;
     hipLaunchKernelGGL(split_sum_nt, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<const f4*>(ws), ns, n4,
-                       reinterpret_cast<f4*>(out), a.outb, (int32_t)M, outb);
+                       reinterpret_cast<f4*>(out), a.outb, ns, (int32_t)M, outb);
     return hipGetLastError();
   }
   const bool pipelined = v == 2 && N % 16 == 0 && a.n0 % 16 == 0 &&
@@ -1506,14 +1771,102 @@ hipError_t nt_run(NTArgs a, int64_t M, int64_t N, int32_t nodes, float* out, flo
   const int64_t n4 = M * N / 4;
   const int64_t blocks = (n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048;
   hipLaunchKernelGGL(split_sum_nt, dim3((unsigned)blocks), dim3(256), 0, st, reinterpret_cast<const f4*>(ws), ns, n4,
-                     reinterpret_cast<f4*>(out), a.outb, (int32_t)M, outb);
+                     reinterpret_cast<f4*>(out), a.outb, ns, (int32_t)M, outb);
   return hipGetLastError();
 }
+// The pre-split-A weight gradient (split_rows + gemm_nt_psa): workspace = [partial tiles (splits > 1)]
+// [dy's packed image, M K 6 bytes][row-sum group partials].  The default (split_nt -1) where C >= 1024
+// and the image is addressable with 32-bit buffer offsets; forced by split_nt 4.  The GEMM alone runs
+// 15-20 % faster than gemm_nt_split_w4_mf16 at every config shape (configs[3]: 281 vs 333 us,
+// 244 TF/s); behind the data gradient in a training step (tools/exp_dy_image.py, HIP graph, the chip at
+// its power limit) the pair gains 3 % at C = 1024 / 2048 (configs[4] 1278 vs 1320 us, [3] 626 vs
+// 648), 1 % at C = 1280 and loses 4 % at C = 512 (the split pass moves 10 bytes per element of dy
+// for a re-split factor of only 2C / 128 = 8 there).
+struct PsaPlan {
+  int ns, G, ngroups;
+  int64_t kchunk, img_off, rs_off, bytes;
+};
+
+bool psa_ok(int64_t M, int64_t ktot) {
+  const int v = mrp_host::tuning().split_nt;
+  return ((v < 0 && M >= 1024) || v == 4) && M % 32 == 0 && ktot % BK == 0 && M * ktot * 6 < kOffMax;
+}
+
+PsaPlan psa_plan(int64_t M, int64_t N, int64_t ktot) {
+  PsaPlan q{};
+  const int64_t tiles = ((M + NTGeo<4>::TM - 1) / NTGeo<4>::TM) * ((N + TN - 1) / TN);
+  q.ns = nt_splits(tiles, ktot, M, N, &q.kchunk);
+  // split_rows: one wave per (32-row block, group of G 16-k steps), ~8192 waves
+  const int64_t KS = ktot / 16, MB = M / 32;
+  int64_t G = (KS * MB + 8191) / 8192;
+  if (G < 1) G = 1;
+  q.G = (int)G;
+  q.ngroups = (int)((KS + G - 1) / G);
+  auto al = [](int64_t v) { return (v + 255) / 256 * 256; };
+  q.img_off = al(q.ns > 1 ? (int64_t)q.ns * M * N * 4 : 0);
+  q.rs_off = al(q.img_off + M * ktot * 6);
+  q.bytes = q.rs_off + (int64_t)q.ngroups * M * 4;
+  return q;
+}
+
+// The pre-split-A GEMM proper: dW (+ db from rparts row-sum partials [M][nparts]) from dy's packed
+// image `img` (split_rows' layout, or written by the data gradient: mrp_compress_bwd_data_split_img);
+// the workspace holds the partial tiles when the plan splits K
+hipError_t psa_gemm(NTArgs a, int64_t M, int64_t N, const u4* img, const float* rparts, int nparts, float* out,
+                    float* outb, void* tiles_ws, hipStream_t st) {
+  using G = NTGeo<4>;
+  const PsaPlan q = psa_plan(M, N, a.ktot);
+  a.ap = img;
+  a.mtiles = (int32_t)((M + G::TM - 1) / G::TM);
+  a.ntiles = (int32_t)((N + TN - 1) / TN);
+  a.kchunk = q.kchunk;
+  a.out = q.ns == 1 ? out : static_cast<float*>(tiles_ws);
+  a.outb = nullptr;
+  a.M = (int32_t)M;
+  a.N = (int32_t)N;
+  const int64_t grid = (int64_t)a.mtiles * a.ntiles * q.ns;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_psa),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(gemm_nt_psa, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (outb != nullptr) {
+    hipLaunchKernelGGL(row_sums, dim3((unsigned)M), dim3(64), 0, st, rparts, nparts, (int32_t)M, outb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (q.ns == 1) return hipSuccess;
+  const int64_t n4 = M * N / 4;
+  const int64_t blocks = (n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048;
+  hipLaunchKernelGGL(split_sum_nt, dim3((unsigned)blocks), dim3(256), 0, st, static_cast<const f4*>(tiles_ws), q.ns,
+                     n4, reinterpret_cast<f4*>(out), nullptr, 0, (int32_t)M, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t nt_run_psa(NTArgs a, int64_t M, int64_t N, int32_t nodes, float* out, float* outb, void* workspace,
+                      int64_t workspace_bytes, hipStream_t st) {
+  a.ktot = (int64_t)nodes * a.P;
+  const PsaPlan q = psa_plan(M, N, a.ktot);
+  if (workspace == nullptr || workspace_bytes < q.bytes || !aligned16(workspace)) return hipErrorInvalidValue;
+  char* ws = static_cast<char*>(workspace);
+  u4* img = reinterpret_cast<u4*>(ws + q.img_off);
+  float* rs = reinterpret_cast<float*>(ws + q.rs_off);
+  const int64_t waves = (M / 32) * q.ngroups;
+  hipLaunchKernelGGL(split_rows, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a.g, a.gs, (int32_t)M, a.P,
+                     a.ktot / 16, q.G, q.ngroups, img, outb != nullptr ? rs : nullptr);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return psa_gemm(a, M, N, img, rs, q.ngroups, out, outb, ws, st);
+}
+
 }  // namespace
 
 extern "C" int64_t mrp_compress_bwd_weight_split_workspace(int32_t num_nodes, int32_t C, int32_t P) {
   if (!nt_split_ok(num_nodes, C, P)) return 0;
-  return nt_workspace(C, 2 * (int64_t)C, (int64_t)num_nodes * P);
+  const int64_t ktot = (int64_t)num_nodes * P;
+  if (psa_ok(C, ktot)) return psa_plan(C, 2 * (int64_t)C, ktot).bytes;
+  return nt_workspace(C, 2 * (int64_t)C, ktot);
 }
 
 extern "C" int mrp_compress_bwd_weight_split(const float* gy, int64_t gy_node_stride, const float* x,
@@ -1545,6 +1898,8 @@ extern "C" int mrp_compress_bwd_weight_split(const float* gy, int64_t gy_node_st
   a.s1s = agg_node_stride;
   a.n0 = C;
   a.P = P;
+  if (psa_ok(M, (int64_t)num_nodes * P))
+    return nt_run_psa(a, M, N, num_nodes, gw, gbias, workspace, workspace_bytes, st);
   return nt_run(a, M, N, num_nodes, gw, gbias, workspace, workspace_bytes, st);
 }
 

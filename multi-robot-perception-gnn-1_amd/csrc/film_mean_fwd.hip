@@ -111,7 +111,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"edge_split_k", &t.edge_split_k, 0, 2},
       {"edge_split_v", &t.edge_split_v, -1, 4},
       {"gemm_split", &t.gemm_split, -1, 7},
-      {"split_nt", &t.split_nt, -1, 3},
+      {"split_nt", &t.split_nt, -1, 4},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {

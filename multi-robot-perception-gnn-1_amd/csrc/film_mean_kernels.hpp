@@ -949,6 +949,65 @@ __device__ __forceinline__ float group_sum(float x) {
   return x;
 }
 
+// Reduce-scatter of 64 values over an aligned group of L = 2^t lanes (L <= 64): on return lane gl of
+// the group holds in v[0 .. 64 / L) the group sums of values [gl 64 / L, (gl + 1) 64 / L).  At each
+// step a lane keeps one half of its current range and sends its partner the other, so the sums cost
+// 64 - 64 / L exchanges instead of the all-reduce's 64 log2 L (group_sum on every value).  Steps run
+// from the group's top lane bit down — xor 32 and xor 16 by ds_bpermute, then row_mirror,
+// row_half_mirror and the two quad perms by DPP: a mirror pairs lanes that differ in the low bits
+// too, but the range a lane holds depends only on the bits above the step's, which a mirror keeps.
+// Each sum is formed on one lane in a fixed order: deterministic.
+template <int CNT, int BIT>
+__device__ __forceinline__ void rs_step(float (&v)[64], int lane) {
+  constexpr int H = CNT / 2;
+  const bool up = (lane >> BIT) & 1;
+#pragma unroll
+  for (int j = 0; j < H; ++j) {  // element j and j + H only: one pass, few values live at once
+    const float send = up ? v[j] : v[j + H];
+    float r;
+    if constexpr (BIT == 5)
+      r = __shfl_xor(send, 32, 64);
+    else if constexpr (BIT == 4)
+      r = __shfl_xor(send, 16, 64);
+    else if constexpr (BIT == 3)
+      r = dpp_mov<0x140>(send);  // row_mirror: i <-> 15 - i
+    else if constexpr (BIT == 2)
+      r = dpp_mov<0x141>(send);  // row_half_mirror: i <-> 7 - i
+    else if constexpr (BIT == 1)
+      r = dpp_mov<0x4E>(send);  // quad_perm [2,3,0,1]
+    else
+      r = dpp_mov<0xB1>(send);  // quad_perm [1,0,3,2]
+    v[j] = (up ? v[j + H] : v[j]) + r;
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void reduce_scatter64(float (&v)[64], int lane) {
+  // the step at lane bit b follows the log2(L) - 1 - b steps above it: 128 2^b / L values left
+  if constexpr (L >= 64) rs_step<128 * 32 / L, 5>(v, lane);
+  if constexpr (L >= 32) rs_step<128 * 16 / L, 4>(v, lane);
+  if constexpr (L >= 16) rs_step<128 * 8 / L, 3>(v, lane);
+  if constexpr (L >= 8) rs_step<128 * 4 / L, 2>(v, lane);
+  if constexpr (L >= 4) rs_step<128 * 2 / L, 1>(v, lane);
+  if constexpr (L >= 2) rs_step<128 / L, 0>(v, lane);
+}
+
+// film_bwd_fused, complete 8-node graphs: reduce-scatter the lane's 64 values (Gram D[i][u] at i 8 + u,
+// S[i] in the diagonal slot) over the group's L lanes, then each lane of an active group stores its
+// 64 / L sums: S[i] to sl[i], D[i][u] to dl[i NTP + u]
+template <int L, int NTP>
+__device__ __forceinline__ void rs_store(float (&vals)[64], int li, bool active, float* sl, float* dl) {
+  constexpr int K = 64 / L;
+  reduce_scatter64<L>(vals, threadIdx.x & 63);
+  if (!active) return;
+  const int gl = li & (L - 1);
+#pragma unroll
+  for (int jj = 0; jj < K; ++jj) {
+    const int idx = gl * K + jj, i = idx >> 3, u = idx & 7;
+    *(i == u ? sl + i : dl + i * NTP + u) = vals[jj];
+  }
+}
+
 // Call f(std::integral_constant<int, L>) with L = lpc: the lane count is wave-uniform but only
 // known at run time, so branch once here rather than once per reduced value (a runtime-width
 // butterfly costs a scalar compare and branch per step per value).
@@ -1141,7 +1200,35 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
         }
       }
     }
-    if (a.want_dgb) {
+    if constexpr (COMPLETE && NT == 8 && VB == 8) {
+      __builtin_amdgcn_sched_barrier(0);  // the sweep's registers are free before the reduction starts
+      // the reference's configuration (complete 8-robot graphs): the 56 Gram values and 8 S values of
+      // the lane (S[i] in the diagonal slot i 8 + i, not an edge) reduce-scattered over the channel
+      // group's lanes (a wave when the plane spans several), each lane then storing its share
+      if (a.want_dgb) {
+        float vals[64];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int u = 0; u < 8; ++u) vals[i * 8 + u] = u == i ? S[i] : D[i][u];
+        // li recomputed from the thread id (lpc is a power of two): keeping it live across the sweep
+        // pushed the PRE2 instantiations past 256 registers
+        const int lir = (int)threadIdx.x & (a.lpc - 1);
+        const int pg = wpc > 1 ? grp * wpc + (lir >> 6) : grp;
+        float* const sl = Sl + pg * SLS;
+        float* const dl = Dl + pg * SZ;
+        const int li = lir;
+        switch (a.lpc) {  // (no lambda: its by-reference captures went to scratch)
+          case 1: rs_store<1, NTP>(vals, li, active, sl, dl); break;
+          case 2: rs_store<2, NTP>(vals, li, active, sl, dl); break;
+          case 4: rs_store<4, NTP>(vals, li, active, sl, dl); break;
+          case 8: rs_store<8, NTP>(vals, li, active, sl, dl); break;
+          case 16: rs_store<16, NTP>(vals, li, active, sl, dl); break;
+          case 32: rs_store<32, NTP>(vals, li, active, sl, dl); break;
+          default: rs_store<64, NTP>(vals, li, active, sl, dl); break;
+        }
+      }
+    } else if (a.want_dgb) {
       // Reduce across the lanes of each channel group (all lanes of the wave take part in the
       // shuffles; inactive groups contribute zeros to their own group).
       with_lanes(a.lpc, [&](auto lanes) {

@@ -42,7 +42,10 @@ struct Tuning {
   // mrp_edge_encoder_fwd_split kernel: -1 per shape, 0 the per-wave hidden layer, 1..4 shared-hidden
   // forms (CB, waves) = (1, 4), (2, 4), (1, 8), (2, 8)
   int edge_split_v = -1;
-  // split-bf16 weight-gradient (NT) kernel: -1 / 3 the 32-k-stage form on 16x16x32 MFMAs (default),
+  // split-bf16 weight-gradient (NT) kernel: 4 (the default where C >= 1024) the compress weight gradient
+  // with dy split once into a packed image (split_rows + gemm_nt_psa) where the image fits 32-bit
+  // offsets, else (and for the encoder's products) 3 (the default below C = 1024): the 32-k-stage form
+  // on 16x16x32 MFMAs splitting both operands;
   // 2 the pipelined 16-k-stage 32x32x16 form (gemm_nt_split3_w4), 1 the 32-k-stage 32x32x16 form
   int split_nt = -1;
   int edge_gemm = 1;  // edge encoder's second Linear: 64 x 64 tiles of 32 x 32 waves on 16x16x4 (0) or 32x32x2 (1) MFMAs

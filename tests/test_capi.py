@@ -189,7 +189,7 @@ def test_tuning_knobs_documented_in_the_header():
                              ("bwd_pre2", 0, 2), ("fwd_regular_split", 0, 1), ("bwd_fused_cap", 1, 64),
                              ("gemm_nn", -1, 5), ("gemm_nt", -1, 5), ("edge_gemm", 0, 1), ("edge_fused", 0, 4),
                              ("edge_split_cb", 0, 2), ("edge_split_k", 0, 2), ("edge_split_v", -1, 4),
-                             ("gemm_split", -1, 7), ("split_nt", -1, 3)):
+                             ("gemm_split", -1, 7), ("split_nt", -1, 4)):
             assert name.encode() in open(os.path.join(ROOT, "include", "mrp_gnn.h"), "rb").read() or \
                 name.startswith("bwd_fused")
             assert lib.mrp_tuning_set(name.encode(), lo) == 0

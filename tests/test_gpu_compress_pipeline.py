@@ -109,14 +109,16 @@ def test_mf16_form_vs_float64(cuda_device, n, C, H, W):
     assert ok, ("grad", errs)
 
 
-@pytest.mark.parametrize("form", [1, 2, 3])
+@pytest.mark.parametrize("form", [1, 2, 3, 4])
 @pytest.mark.parametrize("n,C,H,W", [(16, 64, 8, 8), (10, 128, 16, 16), (64, 256, 8, 8), (7, 160, 4, 8), (2, 32, 32, 32),
-                                     (33, 96, 8, 8), (8, 512, 8, 8), (3, 320, 16, 16), (128, 512, 32, 32)])
+                                     (33, 96, 8, 8), (8, 512, 8, 8), (3, 320, 16, 16), (128, 512, 32, 32),
+                                     (1024, 512, 4, 8), (256, 1280, 8, 8)])
 def test_weight_gradient_forms_vs_float64(cuda_device, form, n, C, H, W):
     """The weight gradient on each NT kernel form (split_nt 1: 32-k stages on 32x32x16 MFMAs, 2: the
-    pipelined 16-k-stage form, 3 (default): 32-k stages on 16x16x32 MFMAs) against float64 with the
-    fp32 yardstick, repeated launches bit-identical; forms 1 and 2 compute the same products in the
-    same order per output (bit-identical dW at equal splits)."""
+    pipelined 16-k-stage form, 3: 32-k stages on 16x16x32 MFMAs, 4 (the default where C >= 1024): form 3 with dy split once
+    into a packed image, split_rows + gemm_nt_psa) against float64 with the fp32 yardstick, repeated
+    launches bit-identical; forms 1 and 2, and forms 3 and 4, compute the same products in the same
+    order per output (bit-identical dW at equal splits; form 4's bias sums dy in other groups)."""
     import stack_ref
     torch.manual_seed(n * 13 + C)
     dev = cuda_device
@@ -128,8 +130,8 @@ def test_weight_gradient_forms_vs_float64(cuda_device, form, n, C, H, W):
     try:
         gw, gb = m.compress.compress_backward_weight(gy, x, a)
         again = m.compress.compress_backward_weight(gy, x, a)
-        if form == 2:
-            assert lib.mrp_tuning_set(b"split_nt", 1) == 0
+        if form in (2, 4):
+            assert lib.mrp_tuning_set(b"split_nt", form - 1) == 0
             assert torch.equal(gw, m.compress.compress_backward_weight(gy, x, a)[0])
     finally:
         lib.mrp_tuning_set(b"split_nt", -1)
@@ -142,3 +144,4 @@ def test_weight_gradient_forms_vs_float64(cuda_device, form, n, C, H, W):
     assert ok, ("gw", errs)
     ok, errs = stack_ref.within(gb, gy.sum((0, 2, 3)), gy.double().sum((0, 2, 3)))
     assert ok, ("gb", errs)
+

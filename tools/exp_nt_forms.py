@@ -1,6 +1,6 @@
 """Kernel lab (not product code): the split-bf16 weight gradient (compress_backward_weight) per BASELINE
 config shape with the 32-k-stage NT kernel (split_nt 1), the pipelined one (split_nt 2) and the
-32-k-stage one on 16x16x32 MFMAs (split_nt 3, lab), HIP-graph
+32-k-stage one on 16x16x32 MFMAs (split_nt 3) and that one with dy pre-split once (split_nt 4), HIP-graph
 timed (bench.time_launches), plus the edge encoder's two backward products at the headline; dW
 outputs compared between the forms (bit-identical at equal splits).
 usage: python tools/exp_nt_forms.py [iters] [forms, e.g. 1,2,3]"""
@@ -14,7 +14,7 @@ import mrp_gnn_amd as mrp  # noqa: E402
 from bench import time_launches  # noqa: E402
 
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-FORMS = tuple(int(v) for v in sys.argv[2].split(",")) if len(sys.argv) > 2 else (1, 2, 3)
+FORMS = tuple(int(v) for v in sys.argv[2].split(",")) if len(sys.argv) > 2 else (3, 4)
 dev = torch.device("cuda:0")
 lib = mrp.load_library()
 cm = mrp.compress
