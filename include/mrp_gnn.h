@@ -303,18 +303,9 @@ int mrp_edge_logits_fwd(const float* h, int32_t num_edges, int32_t C, const floa
                         float* z, void* stream);
 
 /*
- * The edge encoder before its Sigmoid in one launch (dgl/model/models.py:146-149), for inference:
- *   z = relu(pose W1^T + b1) W2^T + b2     pose (num_edges, 9), w1 (C, 9), b1 (C), w2 (2C, C), b2 (2C)
- * The hidden layer is evaluated inside the GEMM's A tiles (bit-identical to mrp_edge_hidden_fwd) and
- * never written; training keeps h for its backward and runs mrp_edge_hidden_fwd + mrp_edge_logits_fwd.
- * Requirements (else hipErrorNotSupported): C % 32 == 0, w1, b1, w2 16-byte aligned, W1 and b1 plus
- * the stage buffers within 160 KiB of LDS (C <= 2816).
- */
-int mrp_edge_encoder_fwd(const float* pose, const float* w1, const float* b1, const float* w2,
-                         const float* b2, int32_t num_edges, int32_t C, float* z, void* stream);
-
-/*
- * The same forward at fp32 accuracy on the bf16 matrix cores (encoder_split.hip): every fp32 operand is
+ * The edge encoder before its Sigmoid in one launch (dgl/model/models.py:146-149),
+ *   z = relu(pose W1^T + b1) W2^T + b2     pose (num_edges, 9), w1 (C, 9), b1 (C), w2 (2C, C), b2 (2C),
+ * at fp32 accuracy on the bf16 matrix cores (encoder_split.hip): every fp32 operand is
  * split exactly into three bf16 parts and each product is the sum of the six partial products whose
  * omitted terms are below 2^-25 of it (error against float64 at or below an fp32 GEMM's); the hidden
  * layer is computed on the matrix cores too (b1 as a tenth input of value 1.0) and never written.
@@ -417,25 +408,22 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * "reset" restores every default.  Geometry: "fwd_lo"/"fwd_hi"/"fwd_cap", "fwd_regular_*",
  * "bwd_fused_*", "bwd_regular_*"; kernel choice: "bwd_regular_mfma" (1, default: the matrix-core
  * backward for MRP_GRAPH_REGULAR graphs of 9..16 nodes), "bwd_complete_mfma" (1, default: the
- * matrix-core backward for complete graphs of 9..16 nodes too; those of <= 8 always run the VALU one), "bwd_mfma_cpw" (channel blocks per wave of the matrix-core
- * backward, 1 or 2), "bwd_pre2" (0 off, 1 on, 2 on unless a grad_x base is given), "fwd_regular_split" (0, default: whole planes); compress GEMM
- * kernel variants "gemm_nn" / "gemm_nt" (-1, default: the per-shape choice; 0..5: compress_gemm.hip's
- * variant table); "edge_gemm" (1, default: mrp_edge_logits_fwd on 32x32x2 MFMAs; 0: 16x16x4); "edge_fused"
- * (mrp_edge_encoder_fwd tile/buffer variant, 0..4); "edge_split_v" (mrp_edge_encoder_fwd_split form: -1,
- * default: per shape; 0: the per-wave hidden layer; 1..4: the hidden layer shared by a workgroup of 4
- * or 8 waves with 1 or 2 column blocks each); "edge_split_cb" (form 0: 32-column
- * blocks per wave, 1 or 2; 0, default: per shape); "edge_split_k" (its hidden blocks over 1 or 2
- * wave sets, 2 only when C % 64 == 0; 0, default: per shape); "gemm_split" (split-bf16 compress
- * forward / data-gradient kernel: -1 per shape (7 where M % 256 == 0, else 2), 2 = 128 rows / 4 waves,
- * 4 = 256 rows / 8 waves with 32-k stages, 5 = 256 rows / 8 waves, pipelined 16-k stages, 6 = two
- * pipelined 128-row / 4-wave workgroups per CU, 7 = 256 rows / 8 waves with 32-k stages on 16x16x32
- * MFMAs; any other value is rejected); "split_nt" (split-bf16
- * weight-gradient kernel of mrp_compress_bwd_weight_split and mrp_edge_encoder_bwd_split: -1 or 3,
- * default: 32-k stages on 16x16x32 MFMAs; 2 = the pipelined 16-k-stage 32x32x16 form where its layout
- * conditions hold; 1 = 32-k stages on 32x32x16; 0 is rejected). */
+ * matrix-core backward for complete graphs of 9..16 nodes too; those of <= 8 always run the VALU
+ * one), "bwd_mfma_cpw" (channel blocks per wave of the matrix-core backward, 1 or 2), "bwd_pre2" (0
+ * off, 1 on, 2 on unless a grad_x base is given), "fwd_regular_split" (0, default: whole planes).
+ * Knobs that name a kernel accept only the kernels the library builds: "edge_split_v"
+ * (mrp_edge_encoder_fwd_split: -1, default: per shape; 1 / 3: the hidden layer shared by a workgroup
+ * of 4 / 8 waves); "gemm_split" (split-bf16 compress forward / data gradient: -1 per shape (7 where
+ * M % 256 == 0, else 2), 2 = 128 rows / 4 waves on 32x32x16 MFMAs, 7 = 256 rows / 8 waves on 16x16x32
+ * MFMAs); "split_nt" (split-bf16 weight gradient of mrp_compress_bwd_weight_split and
+ * mrp_edge_encoder_bwd_split: -1 per shape, 3 = both operands split in the kernel on 16x16x32 MFMAs,
+ * 4 = the compress weight gradient with dy split once (split_rows + gemm_nt_psa; the default where
+ * C >= 1024)).  Round 4's other kernel forms are lab code (tools/lab_*.hip) since ABI 18. */
 int mrp_tuning_set(const char* name, int32_t value);
 
-/* Library identification: ABI version (incremented on signature changes; 17 = this header: v16 plus
+/* Library identification: ABI version (incremented on signature changes; 18 = this header: v17 without
+ * mrp_edge_encoder_fwd (the fp32 one-launch encoder, superseded by mrp_edge_encoder_fwd_split) and
+ * with fewer tuning knobs (only those that select kernels the library builds); 17: v16 plus
  * the split-bf16 training path of the edge encoder (mrp_edge_encoder_fwd_split_train, _bwd_prep,
  * _bwd_split, _bwd_t and their workspaces); 16: v15 plus
  * the split-bf16 weight gradient (mrp_compress_bwd_weight_split + workspace); 15: v14 plus

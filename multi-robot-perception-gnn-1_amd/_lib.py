@@ -38,7 +38,6 @@ EXPORTED_SYMBOLS = (
     "mrp_compress_bwd_weight_split",
     "mrp_edge_hidden_fwd",
     "mrp_edge_logits_fwd",
-    "mrp_edge_encoder_fwd",
     "mrp_edge_encoder_pack_bytes",
     "mrp_edge_encoder_pack",
     "mrp_edge_encoder_fwd_split",
@@ -57,7 +56,7 @@ EXPORTED_SYMBOLS = (
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 17
+ABI_VERSION = 18
 MAX_NODES = 16
 
 HIP_ERROR_NOT_SUPPORTED = 801  # hipErrorNotSupported: a fused path declines this shape
@@ -138,8 +137,6 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_edge_hidden_fwd.restype = ctypes.c_int
     lib.mrp_edge_logits_fwd.argtypes = [_P, _I32, _I32, _P, _P, _P, _P]
     lib.mrp_edge_logits_fwd.restype = ctypes.c_int
-    lib.mrp_edge_encoder_fwd.argtypes = [_P, _P, _P, _P, _P, _I32, _I32, _P, _P]
-    lib.mrp_edge_encoder_fwd.restype = ctypes.c_int
     lib.mrp_edge_encoder_pack_bytes.argtypes = [_I32]
     lib.mrp_edge_encoder_pack_bytes.restype = ctypes.c_int64
     lib.mrp_edge_encoder_pack.argtypes = [_P, _P, _P, _I32, _P, _P]

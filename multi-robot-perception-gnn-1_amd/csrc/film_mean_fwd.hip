@@ -72,7 +72,7 @@ Tuning& tuning() {
 
 extern "C" {
 
-int mrp_abi_version(void) { return 17; }
+int mrp_abi_version(void) { return 18; }
 
 int mrp_tuning_set(const char* name, int32_t value) {
   if (name == nullptr) return hipErrorInvalidValue;
@@ -103,22 +103,18 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"bwd_regular_mfma", &t.bwd_regular_mfma, 0, 1},
       {"bwd_complete_mfma", &t.bwd_complete_mfma, 0, 1},
       {"bwd_mfma_cpw", &t.bwd_mfma_cpw, 1, 2},
-      {"gemm_nn", &t.gemm_nn, -1, 5},
-      {"gemm_nt", &t.gemm_nt, -1, 5},
-      {"edge_gemm", &t.edge_gemm, 0, 1},
-      {"edge_fused", &t.edge_fused, 0, 4},
-      {"edge_split_cb", &t.edge_split_cb, 0, 2},
-      {"edge_split_k", &t.edge_split_k, 0, 2},
-      {"edge_split_v", &t.edge_split_v, -1, 4},
+      {"edge_split_v", &t.edge_split_v, -1, 3},
       {"gemm_split", &t.gemm_split, -1, 7},
       {"split_nt", &t.split_nt, -1, 4},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {
       if (value < k.lo || value > k.hi) return hipErrorInvalidValue;
-      // gemm_split names a kernel: -1 (per shape), 2, 4, 5, 6 or 7 (compress_split.hip); no other value means one
-      if (k.field == &t.gemm_split && (value == 0 || value == 1 || value == 3)) return hipErrorInvalidValue;
-      if (k.field == &t.split_nt && value == 0) return hipErrorInvalidValue;
+      // knobs that name kernels accept only the product's: gemm_split -1 (per shape), 2 or 7;
+      // split_nt -1 (per shape), 3 or 4 (compress_split.hip; round 4's other forms: tools/lab_forms.hip)
+      if (k.field == &t.gemm_split && value != -1 && value != 2 && value != 7) return hipErrorInvalidValue;
+      if (k.field == &t.split_nt && value != -1 && value != 3 && value != 4) return hipErrorInvalidValue;
+      if (k.field == &t.edge_split_v && value != -1 && value != 1 && value != 3) return hipErrorInvalidValue;
       *k.field = value;
       return hipSuccess;
     }

@@ -32,23 +32,16 @@ struct Tuning {
   int bwd_complete_mfma = 1;
   int bwd_mfma_cpw = 2;  // film_bwd_mfma: 16-row blocks per wave (1 or 2)
 
-  // compress GEMMs (compress_gemm.hip): kernel variant of the forward / data-gradient product (NN) and
-  // of the weight-gradient product (NT); see the variant table there
-  int gemm_nn = -1, gemm_nt = -1;  // -1: the per-shape default
-  int edge_fused = 2;  // mrp_edge_encoder_fwd variant (compress_gemm.hip MRP_ENC_VARIANTS)
-  int gemm_split = -1;  // split-bf16 compress GEMM: -1 per shape, 2 (128-row workgroups) or 4 (256-row)
-  int edge_split_cb = 0;  // mrp_edge_encoder_fwd_split: 32-column blocks per wave (1 or 2; 0 per shape)
-  int edge_split_k = 0;   // mrp_edge_encoder_fwd_split: hidden blocks over 1 or 2 wave sets (0 per shape)
-  // mrp_edge_encoder_fwd_split kernel: -1 per shape, 0 the per-wave hidden layer, 1..4 shared-hidden
-  // forms (CB, waves) = (1, 4), (2, 4), (1, 8), (2, 8)
+  // split-bf16 compress forward / data gradient (compress_split.hip): -1 per shape, 7 (256-row
+  // workgroups on 16x16x32 MFMAs, where M % 256 == 0) or 2 (128-row workgroups on 32x32x16)
+  int gemm_split = -1;
+  // mrp_edge_encoder_fwd_split (encoder_split.hip): -1 per shape, 1 = 4 waves, 3 = 8 waves per workgroup
   int edge_split_v = -1;
   // split-bf16 weight-gradient (NT) kernel: 4 (the default where C >= 1024) the compress weight gradient
   // with dy split once into a packed image (split_rows + gemm_nt_psa) where the image fits 32-bit
   // offsets, else (and for the encoder's products) 3 (the default below C = 1024): the 32-k-stage form
-  // on 16x16x32 MFMAs splitting both operands;
-  // 2 the pipelined 16-k-stage 32x32x16 form (gemm_nt_split3_w4), 1 the 32-k-stage 32x32x16 form
+  // on 16x16x32 MFMAs splitting both operands
   int split_nt = -1;
-  int edge_gemm = 1;  // edge encoder's second Linear: 64 x 64 tiles of 32 x 32 waves on 16x16x4 (0) or 32x32x2 (1) MFMAs
 };
 Tuning& tuning();
 

@@ -56,11 +56,10 @@ _LOGITS_PATH = "split"
 
 def set_logits_path(path: str) -> None:
     """"split" (default): ``mrp_edge_encoder_fwd_split`` (split-bf16 matrix cores) when no gradient is
-    wanted, else as "hip"; "fused": the fp32-MFMA one-launch ``mrp_edge_encoder_fwd`` likewise;
-    "hip": ``mrp_edge_hidden_fwd`` + ``mrp_edge_logits_fwd``; "library": the hidden kernel +
-    ``torch.addmm`` (comparison runs)."""
+    wanted and the split training path otherwise; "hip": ``mrp_edge_hidden_fwd`` +
+    ``mrp_edge_logits_fwd`` (fp32 MFMA); "library": the hidden kernel + ``torch.addmm`` (comparison runs)."""
     global _LOGITS_PATH
-    if path not in ("split", "fused", "hip", "library"):
+    if path not in ("split", "hip", "library"):
         raise ValueError(f"unknown logits path {path!r}")
     _LOGITS_PATH = path
 
@@ -119,24 +118,6 @@ def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
     if code == _lib.HIP_ERROR_NOT_SUPPORTED:
         return None
     _lib.check(code, "mrp_edge_encoder_fwd_split")
-    return z
-
-
-def encoder_forward_fused(pose, w1, b1, w2, b2) -> torch.Tensor:
-    """z = relu(pose W1^T + b1) W2^T + b2, (E, 2C), in one launch (``mrp_edge_encoder_fwd``); None
-    when the kernel declines the shape."""
-    E, C = pose.shape[0], w1.shape[0]
-    if not pose.is_cuda:
-        raise RuntimeError("mrp_gnn: the edge encoder kernel runs only on the GPU; no CPU fallback")
-    pose, w1, b1, w2, b2 = (t.detach().contiguous().float() for t in (pose, w1, b1, w2, b2))
-    z = torch.empty((E, 2 * C), device=pose.device, dtype=torch.float32)
-    lib = _lib.load_library()
-    with torch.cuda.device(pose.device):
-        code = lib.mrp_edge_encoder_fwd(_ptr(pose), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), E, C, _ptr(z),
-                                        ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream))
-    if code == _lib.HIP_ERROR_NOT_SUPPORTED:
-        return None
-    _lib.check(code, "mrp_edge_encoder_fwd")
     return z
 
 
@@ -250,7 +231,7 @@ class EdgeEncoderFunction(torch.autograd.Function):
                 db2 if need[4] else None)
 
 
-#: calls per encoder path ("split": mrp_edge_encoder_fwd_split, "fused": mrp_edge_encoder_fwd,
+#: calls per encoder path ("split": mrp_edge_encoder_fwd_split,
 #: "split_train": EdgeEncoderSplitFunction, "autograd": EdgeEncoderFunction) — lets tests assert which
 #: kernels a forward actually ran
 PATH_COUNTS = collections.Counter()
@@ -396,11 +377,6 @@ def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Te
         z = encoder_forward_split(pose, l1, l2)
         if z is not None:
             PATH_COUNTS["split"] += 1
-            return z
-    if _LOGITS_PATH == "fused" and inference:
-        z = encoder_forward_fused(*params)
-        if z is not None:
-            PATH_COUNTS["fused"] += 1
             return z
     C = l1.weight.shape[0]
     if _LOGITS_PATH == "split" and split_train_supported(pose.shape[0], C) and l1.bias is not None \

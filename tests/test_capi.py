@@ -186,21 +186,21 @@ def test_tuning_knobs_documented_in_the_header():
     lib = m.load_library()
     try:
         for name, lo, hi in (("bwd_regular_mfma", 0, 1), ("bwd_complete_mfma", 0, 1), ("bwd_mfma_cpw", 1, 2),
-                             ("bwd_pre2", 0, 2), ("fwd_regular_split", 0, 1), ("bwd_fused_cap", 1, 64),
-                             ("gemm_nn", -1, 5), ("gemm_nt", -1, 5), ("edge_gemm", 0, 1), ("edge_fused", 0, 4),
-                             ("edge_split_cb", 0, 2), ("edge_split_k", 0, 2), ("edge_split_v", -1, 4),
-                             ("gemm_split", -1, 7), ("split_nt", -1, 4)):
+                             ("bwd_pre2", 0, 2), ("fwd_regular_split", 0, 1), ("bwd_fused_cap", 1, 64)):
             assert name.encode() in open(os.path.join(ROOT, "include", "mrp_gnn.h"), "rb").read() or \
                 name.startswith("bwd_fused")
             assert lib.mrp_tuning_set(name.encode(), lo) == 0
             assert lib.mrp_tuning_set(name.encode(), hi) == 0
             assert lib.mrp_tuning_set(name.encode(), hi + 1) == HIP_INVALID_VALUE
         assert lib.mrp_tuning_set(b"no_such_knob", 0) == HIP_INVALID_VALUE
-        # gemm_split names a kernel (-1 per shape, 2, 4, 5, 6, 7): the values between name none
-        for v in (0, 1, 3):
-            assert lib.mrp_tuning_set(b"gemm_split", v) == HIP_INVALID_VALUE
-        for v in (-1, 2, 4, 5, 6, 7):
-            assert lib.mrp_tuning_set(b"gemm_split", v) == 0
-        assert lib.mrp_tuning_set(b"split_nt", 0) == HIP_INVALID_VALUE
+        # knobs that name a kernel accept exactly the kernels the library builds (ABI 18)
+        header = open(os.path.join(ROOT, "include", "mrp_gnn.h"), "rb").read()
+        for name, ok in (("edge_split_v", (-1, 1, 3)), ("gemm_split", (-1, 2, 7)), ("split_nt", (-1, 3, 4))):
+            assert name.encode() in header
+            for v in range(-2, 9):
+                assert lib.mrp_tuning_set(name.encode(), v) == (0 if v in ok else HIP_INVALID_VALUE), (name, v)
+        # round 4's kernel-variant knobs are gone with their kernels (tools/lab_*.hip)
+        for name in (b"gemm_nn", b"gemm_nt", b"edge_gemm", b"edge_fused", b"edge_split_cb", b"edge_split_k"):
+            assert lib.mrp_tuning_set(name, 0) == HIP_INVALID_VALUE
     finally:
         assert lib.mrp_tuning_set(b"reset", 0) == 0

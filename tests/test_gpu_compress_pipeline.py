@@ -1,14 +1,12 @@
-"""The split-bf16 compress forward / data-gradient kernel forms (``csrc/compress_split.hip``; knob
-``gemm_split``): 2 = 128-row workgroups, 4 = 256-row with 32-k stages, 5 = the pipelined 256-row form
-(16-k stages in a ring of four LDS buffers, both operands by LDS-DMA with counted waits, the default
-where M % 256 == 0 before form 7), 6 = two pipelined 128-row workgroups per CU, 7 = 256-row 32-k
-stages on 16x16x32 MFMAs (the default where M % 256 == 0).  Forms 2, 4, 5 and 6 accumulate the same
-partial products in the same k order, so their outputs must be bit-identical — across ragged M and
-column tails, the shortest K (two 16-k stages), planes smaller than a column tile — and every launch
-of one kernel must repeat the last bit for bit at a BASELINE config size (the guard against an
-LDS-DMA ordering race: a read that overtakes the DMA it depends on gives rare, shifting errors).
-Form 7 sums 32 k per MFMA instead of 16, so it is held to float64 with the fp32 yardstick here (the
-default path's accuracy is tests/test_gpu_compress_gemm.py's)."""
+"""The split-bf16 compress kernel forms the library builds (``csrc/compress_split.hip``): forward / data
+gradient (knob ``gemm_split``): 2 = 128-row workgroups on 32x32x16 MFMAs (the fallback where M % 256 != 0),
+7 = 256-row workgroups on 16x16x32 MFMAs (the default where M % 256 == 0) — each forced on every shape
+and held to float64 with the fp32 yardstick, across ragged M and column tails, the shortest K (two 16-k
+stages) and planes smaller than a column tile; every launch of a kernel must repeat the last bit for bit
+at a BASELINE config size (the guard against an LDS-DMA ordering race: a read that overtakes the DMA it
+depends on gives rare, shifting errors).  Weight gradient (knob ``split_nt``): 3 = both operands split
+in the kernel, 4 = dy split once (split_rows + gemm_nt_psa), bit-identical dW at the same split.
+Round 4's other forms are lab code (tools/lab_forms.hip)."""
 import contextlib
 
 import pytest
@@ -18,7 +16,6 @@ import mrp_gnn_amd as m
 
 pytestmark = pytest.mark.gpu
 
-FORMS = (2, 4, 5, 6)
 
 
 @contextlib.contextmanager
@@ -34,29 +31,7 @@ def _form(v):
         m.compress.set_compress_path(prev)
 
 
-@pytest.mark.parametrize("n,C,H,W", [(3, 32, 2, 2), (5, 64, 4, 4), (7, 160, 4, 8), (2, 256, 8, 8), (9, 288, 2, 6),
-                                     (33, 96, 8, 8), (4, 512, 16, 16), (1, 256, 1, 4), (17, 320, 4, 4)])
-def test_forms_bit_identical(cuda_device, n, C, H, W):
-    torch.manual_seed(n * 7 + C)
-    dev = cuda_device
-    w = torch.randn(C, 2 * C, 1, 1, device=dev) / (2 * C) ** 0.5
-    b = torch.randn(C, device=dev)
-    x, a, gy = (torch.randn(n, C, H, W, device=dev) for _ in range(3))
-    outs = []
-    for v in FORMS:
-        with _form(v):
-            y = m.compress.compress_forward(w, b, x, a)
-            gx, ga = m.compress.compress_backward_data(w, gy)
-        torch.cuda.synchronize()
-        outs.append((v, y, gx, ga))
-    v0, y0, gx0, ga0 = outs[0]
-    for v, y, gx, ga in outs[1:]:
-        assert torch.equal(y, y0), (v, float((y - y0).abs().max()))
-        assert torch.equal(gx, gx0), (v, float((gx - gx0).abs().max()))
-        assert torch.equal(ga, ga0), (v, float((ga - ga0).abs().max()))
-
-
-@pytest.mark.parametrize("form", [5, 6, 7])
+@pytest.mark.parametrize("form", [2, 7])
 def test_config1_size_repeats_bit_identical(cuda_device, form):
     """configs[1]'s layer shape (128 nodes, C = 512, 32 x 32): forward, data gradient and weight
     gradient launched repeatedly on the same inputs give the same bits every time."""
@@ -81,17 +56,19 @@ def test_config1_size_repeats_bit_identical(cuda_device, form):
 @pytest.mark.parametrize("n,C,H,W", [(3, 32, 2, 2), (5, 64, 4, 4), (7, 160, 4, 8), (2, 256, 8, 8), (9, 288, 2, 6),
                                      (33, 96, 8, 8), (4, 512, 16, 16), (1, 256, 1, 4), (17, 320, 4, 4),
                                      (16, 1280, 8, 8)])
-def test_mf16_form_vs_float64(cuda_device, n, C, H, W):
-    """Form 7 (16x16x32 MFMAs) — the default where M % 256 == 0, forced here on every shape (ragged M
-    tiles and column tails, the shortest K, planes smaller than a column tile): forward and data
-    gradient against float64 with the fp32 yardstick, repeated launches bit-identical."""
+@pytest.mark.parametrize("form", [2, 7])
+def test_forms_vs_float64(cuda_device, form, n, C, H, W):
+    """Form 7 (16x16x32 MFMAs, the default where M % 256 == 0) and form 2 (32x32x16, the fallback),
+    each forced on every shape (ragged M tiles and column tails, the shortest K, planes smaller than a
+    column tile): forward and data gradient against float64 with the fp32 yardstick, repeated launches
+    bit-identical."""
     import stack_ref
     torch.manual_seed(n * 5 + C)
     dev = cuda_device
     w = torch.randn(C, 2 * C, 1, 1, device=dev) / (2 * C) ** 0.5
     b = torch.randn(C, device=dev)
     x, a, gy = (torch.randn(n, C, H, W, device=dev) for _ in range(3))
-    with _form(7):
+    with _form(form):
         y = m.compress.compress_forward(w, b, x, a)
         gx, ga = m.compress.compress_backward_data(w, gy)
         assert torch.equal(y, m.compress.compress_forward(w, b, x, a))
@@ -109,16 +86,16 @@ def test_mf16_form_vs_float64(cuda_device, n, C, H, W):
     assert ok, ("grad", errs)
 
 
-@pytest.mark.parametrize("form", [1, 2, 3, 4])
+@pytest.mark.parametrize("form", [3, 4])
 @pytest.mark.parametrize("n,C,H,W", [(16, 64, 8, 8), (10, 128, 16, 16), (64, 256, 8, 8), (7, 160, 4, 8), (2, 32, 32, 32),
                                      (33, 96, 8, 8), (8, 512, 8, 8), (3, 320, 16, 16), (128, 512, 32, 32),
                                      (1024, 512, 4, 8), (256, 1280, 8, 8)])
 def test_weight_gradient_forms_vs_float64(cuda_device, form, n, C, H, W):
-    """The weight gradient on each NT kernel form (split_nt 1: 32-k stages on 32x32x16 MFMAs, 2: the
-    pipelined 16-k-stage form, 3: 32-k stages on 16x16x32 MFMAs, 4 (the default where C >= 1024): form 3 with dy split once
-    into a packed image, split_rows + gemm_nt_psa) against float64 with the fp32 yardstick, repeated
-    launches bit-identical; forms 1 and 2, and forms 3 and 4, compute the same products in the same
-    order per output (bit-identical dW at equal splits; form 4's bias sums dy in other groups)."""
+    """The weight gradient on each NT kernel form (split_nt 3: 32-k stages on 16x16x32 MFMAs, both
+    operands split in the kernel; 4 (the default where C >= 1024): dy split once into a packed image,
+    split_rows + gemm_nt_psa) against float64 with the fp32 yardstick, repeated launches bit-identical;
+    forms 3 and 4 compute the same products in the same order per output (bit-identical dW at equal
+    splits; form 4's bias sums dy in other groups)."""
     import stack_ref
     torch.manual_seed(n * 13 + C)
     dev = cuda_device
@@ -130,8 +107,8 @@ def test_weight_gradient_forms_vs_float64(cuda_device, form, n, C, H, W):
     try:
         gw, gb = m.compress.compress_backward_weight(gy, x, a)
         again = m.compress.compress_backward_weight(gy, x, a)
-        if form in (2, 4):
-            assert lib.mrp_tuning_set(b"split_nt", form - 1) == 0
+        if form == 4:
+            assert lib.mrp_tuning_set(b"split_nt", 3) == 0
             assert torch.equal(gw, m.compress.compress_backward_weight(gy, x, a)[0])
     finally:
         lib.mrp_tuning_set(b"split_nt", -1)

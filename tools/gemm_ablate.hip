@@ -2,7 +2,7 @@
 // gemm_nn_split3_body's ABL bits) at the configs[3] forward shape, timed with hipEvents.  Outputs of
 // ablated runs are garbage by design; only ABL = 0 is checked (against the library's kernel).
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I include tools/gemm_ablate.hip -o tools/bin/gemm_ablate
-#include "../multi-robot-perception-gnn-1_amd/csrc/compress_split.hip"
+#include "lab_forms.hip"
 
 #include <algorithm>
 #include <cstdio>
