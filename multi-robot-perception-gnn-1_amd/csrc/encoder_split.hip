@@ -183,7 +183,7 @@ struct FwdArgs {
 // The next round's X runs after the current round's z (its W1 loads issued before), so with two
 // waves per SIMD one wave's VALU split runs beside the other's MFMAs.
 // ------------------------------------------------------------------------------------------------
-template <int CB, int NWV, int ABL = 0>  // ABL: lab ablation bits (tools/enc_ablate.hip; 0 in the library)
+template <int CB, int NWV, int ABL = 0, bool ALLX = false>  // ABL: lab ablation bits (tools/enc_ablate.hip; 0 here)
 __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
   extern __shared__ u4 lds_all[];
   const int HB = a.C / 32;
@@ -241,15 +241,16 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
       }
   };
   // X of hidden block hb, ReLU'd and split, into LDS slot (buf, w)
-  u4 w1f[3];
-  auto load_w1 = [&](int hb) {
+  u4 w1f[3], w1g[3];
+  auto load_w1_into = [&](int hb, u4 (&dst)[3]) {
 #pragma unroll
-    for (int p = 0; p < 3; ++p) w1f[p] = img[(int64_t)(min(hb, HB - 1) * 3 + p) * 64 + lane];
+    for (int p = 0; p < 3; ++p) dst[p] = img[(int64_t)(min(hb, HB - 1) * 3 + p) * 64 + lane];
   };
-  auto x_store = [&](int buf, int hbx) {
+  auto load_w1 = [&](int hb) { load_w1_into(hb, w1f); };
+  auto x_store_from = [&](int buf, int hbx, const u4 (&wsrc)[3]) {
     bf8 wa[3];
 #pragma unroll
-    for (int p = 0; p < 3; ++p) wa[p] = as_bf8(w1f[p]);
+    for (int p = 0; p < 3; ++p) wa[p] = as_bf8(wsrc[p]);
     f16v X;
 #pragma unroll
     for (int i = 0; i < 16; ++i) X[i] = 0.f;
@@ -276,6 +277,7 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
       for (int p = 0; p < 3; ++p) slot[(s2 * 3 + p) * 64] = as_u4(hp[p]);
     }
   };
+  auto x_store = [&](int buf, int hbx) { x_store_from(buf, hbx, w1f); };
   f16v Z[CB], ZL[CB];
 #pragma unroll
   for (int c = 0; c < CB; ++c)
@@ -312,11 +314,32 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
   // blocks take the sets in a fixed order
   static_assert(NWV % 4 == 0, "four W2 sets per round");
   W2F f0, f1, f2, f3;
+  // every hidden block fits the two slot sets (HB <= 2 NWV: C <= 512 with 8 waves): all of X first — each
+  // wave computes blocks w and w + NWV — one barrier, then z straight through all HB blocks with no
+  // further barrier or X in between (the rounds below put a barrier and a VALU split phase between
+  // every NWV blocks, with both waves of a SIMD in the split at the same time)
+  constexpr bool allx = ALLX;  // the launcher's choice: HB <= 2 NWV
   load_w1(w);
+  if (allx && w + NWV < HB) load_w1_into(w + NWV, w1g);
   load_w2(0, f0);
   if (1 < HB) load_w2(1, f1);
   if (2 < HB) load_w2(2, f2);
   x_store(0, w);
+  if constexpr (allx) {
+    if (w + NWV < HB) x_store_from(1, w + NWV, w1g);
+    __syncthreads();
+#pragma unroll 1
+    for (int hb = 0; hb < HB; hb += 4) {
+      if (hb + 3 < HB) load_w2(hb + 3, f3);
+      z_block(hb / NWV, hb % NWV, f0);
+      if (hb + 4 < HB) load_w2(hb + 4, f0);
+      if (hb + 1 < HB) z_block((hb + 1) / NWV, (hb + 1) % NWV, f1);
+      if (hb + 5 < HB) load_w2(hb + 5, f1);
+      if (hb + 2 < HB) z_block((hb + 2) / NWV, (hb + 2) % NWV, f2);
+      if (hb + 6 < HB) load_w2(hb + 6, f2);
+      if (hb + 3 < HB) z_block((hb + 3) / NWV, (hb + 3) % NWV, f3);
+    }
+  } else {
   __syncthreads();
 #pragma unroll 1
   for (int rd = 0; rd < rounds; ++rd) {
@@ -338,6 +361,7 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
     if (more) x_store(buf ^ 1, (rd + 1) * NWV + w);  // slot buf ^ 1: last read in round rd - 1, before the last barrier
     if (!(ABL & 4)) __syncthreads();
   }
+  }
   // epilogue: accumulator register i of lane (r, hh) is edge e0 + (i & 3) + 8 (i >> 2) + 4 hh, column r
   const int N = 2 * a.C;
 #pragma unroll
@@ -356,6 +380,8 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
 
 __global__ void __launch_bounds__(256) encoder2_cb1_w4(FwdArgs a) { encoder2_body<1, 4>(a); }
 __global__ void __launch_bounds__(512) encoder2_cb1_w8(FwdArgs a) { encoder2_body<1, 8>(a); }
+__global__ void __launch_bounds__(256) encoder2_cb1_w4_allx(FwdArgs a) { encoder2_body<1, 4, 0, true>(a); }
+__global__ void __launch_bounds__(512) encoder2_cb1_w8_allx(FwdArgs a) { encoder2_body<1, 8, 0, true>(a); }
 
 template <int CB, int NWV>
 hipError_t launch2_cfg(void (*kern)(FwdArgs), const FwdArgs& a, hipStream_t st) {
@@ -369,7 +395,10 @@ hipError_t launch2_cfg(void (*kern)(FwdArgs), const FwdArgs& a, hipStream_t st) 
 }
 
 hipError_t launch_fwd2(int nwv, const FwdArgs& a, hipStream_t st) {
-  return nwv == 8 ? launch2_cfg<1, 8>(encoder2_cb1_w8, a, st) : launch2_cfg<1, 4>(encoder2_cb1_w4, a, st);
+  const bool allx = a.C / 32 <= 2 * nwv && mrp_host::tuning().edge_allx;  // every X before z (encoder2_body)
+  if (nwv == 8)
+    return allx ? launch2_cfg<1, 8>(encoder2_cb1_w8_allx, a, st) : launch2_cfg<1, 8>(encoder2_cb1_w8, a, st);
+  return allx ? launch2_cfg<1, 4>(encoder2_cb1_w4_allx, a, st) : launch2_cfg<1, 4>(encoder2_cb1_w4, a, st);
 }
 
 // the form per shape (mrp_tuning_set "edge_split_v": 3 = 8 waves, 1 = 4 waves per workgroup): 8 waves

@@ -104,6 +104,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"bwd_complete_mfma", &t.bwd_complete_mfma, 0, 1},
       {"bwd_mfma_cpw", &t.bwd_mfma_cpw, 1, 2},
       {"edge_split_v", &t.edge_split_v, -1, 3},
+      {"edge_allx", &t.edge_allx, 0, 1},
       {"gemm_split", &t.gemm_split, -1, 7},
       {"split_nt", &t.split_nt, -1, 4},
   };
