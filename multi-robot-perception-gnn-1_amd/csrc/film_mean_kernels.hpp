@@ -995,17 +995,16 @@ __device__ __forceinline__ void reduce_scatter64(float (&v)[64], int lane) {
 // film_bwd_fused, complete 8-node graphs: reduce-scatter the lane's 64 values (Gram D[i][u] at i 8 + u,
 // S[i] in the diagonal slot) over the group's L lanes, then each lane of an active group stores its
 // 64 / L sums: S[i] to sl[i], D[i][u] to dl[i NTP + u]
+// film_bwd_fused, complete 8-node graphs, planes of >= 64 lanes: reduce-scatter the lane's 64 values
+// (Gram D[i][u] at i 8 + u, S[i] in the diagonal slot) over the wave, then lane l of an active group
+// stores sum l: S[i] to sl[i], D[i][u] to dl[i NTP + u]
 template <int L, int NTP>
 __device__ __forceinline__ void rs_store(float (&vals)[64], int li, bool active, float* sl, float* dl) {
-  constexpr int K = 64 / L;
+  static_assert(L == 64, "one sum per lane");
   reduce_scatter64<L>(vals, threadIdx.x & 63);
   if (!active) return;
-  const int gl = li & (L - 1);
-#pragma unroll
-  for (int jj = 0; jj < K; ++jj) {
-    const int idx = gl * K + jj, i = idx >> 3, u = idx & 7;
-    *(i == u ? sl + i : dl + i * NTP + u) = vals[jj];
-  }
+  const int i = (li & 63) >> 3, u = li & 7;
+  *(i == u ? sl + i : dl + i * NTP + u) = vals[0];
 }
 
 // Call f(std::integral_constant<int, L>) with L = lpc: the lane count is wave-uniform but only
@@ -1200,12 +1199,16 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
         }
       }
     }
+    bool reduced = false;
     if constexpr (COMPLETE && NT == 8 && VB == 8) {
-      __builtin_amdgcn_sched_barrier(0);  // the sweep's registers are free before the reduction starts
-      // the reference's configuration (complete 8-robot graphs): the 56 Gram values and 8 S values of
-      // the lane (S[i] in the diagonal slot i 8 + i, not an edge) reduce-scattered over the channel
-      // group's lanes (a wave when the plane spans several), each lane then storing its share
-      if (a.want_dgb) {
+      // the reference's configuration (complete 8-robot graphs) on planes of >= 64 lanes (32 x 32): the
+      // 56 Gram values and 8 S values of the lane (S[i] in the diagonal slot i 8 + i, not an edge)
+      // reduce-scattered over the wave, each lane then storing one sum — 63 exchanges instead of the
+      // all-reduce's 384 and one store instead of 64 from lane 0 (tools/ab_libs.py: headline backward
+      // 278.7 vs 281.8 us, configs[1] 145.0 vs 149.0).  At 8 lanes per plane (8 x 8) the all-reduce
+      // below stays: the reduce-scatter measured 4 % slower there (configs[2] 60.0 vs 57.6 us).
+      if (a.want_dgb && a.lpc >= 64) {
+        __builtin_amdgcn_sched_barrier(0);  // the sweep's registers are free before the reduction starts
         float vals[64];
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -1215,20 +1218,11 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
         // pushed the PRE2 instantiations past 256 registers
         const int lir = (int)threadIdx.x & (a.lpc - 1);
         const int pg = wpc > 1 ? grp * wpc + (lir >> 6) : grp;
-        float* const sl = Sl + pg * SLS;
-        float* const dl = Dl + pg * SZ;
-        const int li = lir;
-        switch (a.lpc) {  // (no lambda: its by-reference captures went to scratch)
-          case 1: rs_store<1, NTP>(vals, li, active, sl, dl); break;
-          case 2: rs_store<2, NTP>(vals, li, active, sl, dl); break;
-          case 4: rs_store<4, NTP>(vals, li, active, sl, dl); break;
-          case 8: rs_store<8, NTP>(vals, li, active, sl, dl); break;
-          case 16: rs_store<16, NTP>(vals, li, active, sl, dl); break;
-          case 32: rs_store<32, NTP>(vals, li, active, sl, dl); break;
-          default: rs_store<64, NTP>(vals, li, active, sl, dl); break;
-        }
+        rs_store<64, NTP>(vals, lir, active, Sl + pg * SLS, Dl + pg * SZ);
+        reduced = true;
       }
-    } else if (a.want_dgb) {
+    }
+    if (!reduced && a.want_dgb) {
       // Reduce across the lanes of each channel group (all lanes of the wave take part in the
       // shuffles; inactive groups contribute zeros to their own group).
       with_lanes(a.lpc, [&](auto lanes) {

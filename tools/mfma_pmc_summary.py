@@ -19,7 +19,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WHAT = {
     "gemm_fwd": "split-bf16 compress forward, configs[3] layer shape (64 nodes, C=2048, 8x8): M=2048 N=4096 K=4096",
     "gemm_dgrad": "split-bf16 compress data gradient, same shape: M=4096 N=4096 K=2048",
-    "gemm_wgrad": "split-bf16 compress weight gradient, same shape: M=2048 N=4096 K=4096 (split-K)",
+    "gemm_wgrad": "split-bf16 compress weight gradient, same shape: M=2048 N=4096 K=4096, the default form at "
+                  "C >= 1024: dy split once (split_rows, not counted) + gemm_nt_psa",
+    "gemm_wgrad3": "split-bf16 compress weight gradient, same shape, both operands split in the kernel "
+                   "(gemm_nt_split_w4_mf16, the round-4 default)",
     "encoder": "split-bf16 edge encoder forward (shared-hidden form), headline shape E=1792 C=512",
 }
 
@@ -40,13 +43,14 @@ def load(path, regex):
 def main():
     src, rnd = sys.argv[1], sys.argv[2]
     out = {"round": rnd, "method": __doc__.split("\n\n", 2)[2].strip(), "records": {}}
-    for name, regex in (("gemm_fwd", "gemm_n"), ("gemm_dgrad", "gemm_n"), ("gemm_wgrad", "gemm_n"), ("encoder", "encoder")):
+    for name, regex in (("gemm_fwd", "gemm_n"), ("gemm_dgrad", "gemm_n"), ("gemm_wgrad", "gemm_n"),
+                        ("gemm_wgrad3", "gemm_n"), ("encoder", "encoder")):
         path = os.path.join(src, "pmc_" + name, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
         per, span = load(path, regex)
         ids = sorted(per)[1:] or sorted(per)
-        if name == "gemm_wgrad":  # the split-K sum kernel does not match "gemm_n"; only the product
+        if name.startswith("gemm_wgrad"):  # the split-K sum kernel does not match "gemm_n"; only the product
             ids = [d for d in ids if "gemm_nt" in span[d][2]] or ids
         n = len(ids)
         c = {k: sum(per[d].get(k, 0.0) for d in ids) / n for k in per[ids[0]]}

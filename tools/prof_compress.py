@@ -1,6 +1,8 @@
 """Profiling driver (not product code): the split-bf16 compress forward at the configs[3] layer shape
 (64 nodes, C=2048, 8x8), N launches, for one rocprofv3 --kernel-trace or --pmc pass.
-Usage: python tools/prof_compress.py [launches] [op: fwd|dgrad|wgrad]"""
+Usage: python tools/prof_compress.py [launches] [op: fwd|dgrad|wgrad|wgrad3]  (wgrad: the default weight
+gradient — at C = 2048 dy split once, split_rows + gemm_nt_psa; wgrad3: both operands split in the
+kernel, gemm_nt_split_w4_mf16)"""
 import os
 import sys
 
@@ -18,6 +20,8 @@ w = torch.randn(C, 2 * C, 1, 1, device=dev) / (2 * C) ** 0.5
 b = torch.randn(C, device=dev)
 x, a, gy = (torch.randn(n, C, H, H, device=dev) for _ in range(3))
 cm = mrp.compress
+if op == "wgrad3":
+    assert mrp.load_library().mrp_tuning_set(b"split_nt", 3) == 0
 for _ in range(n_launch):
     if op == "fwd":
         cm.compress_forward(w, b, x, a)

@@ -35,7 +35,7 @@ pass SQ1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_
 pass SQ2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS
 pass GRBM GRBM_GUI_ACTIVE GRBM_COUNT
 # matrix-core kernels: the split-bf16 compress GEMMs (configs[3] layer shape) and the edge encoder
-for op in fwd dgrad wgrad; do
+for op in fwd dgrad wgrad wgrad3; do
   timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES \
     --kernel-include-regex "gemm_n" -d "$OUT/pmc_gemm_$op" -o run --output-format csv -- python3 tools/prof_compress.py 5 $op > "$OUT/pmc_gemm_$op.log" 2>&1
 done
