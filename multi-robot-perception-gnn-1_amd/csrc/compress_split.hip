@@ -370,25 +370,46 @@ __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
         }
       }
     }
-    // accumulator register r of lane (r16, qq) of tile (mi, ni): row 16 mi + 4 qq + r, column 16 ni + r16
+    // Epilogue.  Accumulator register r of lane (r16, qq) of tile (mi, ni): row 16 mi + 4 qq + r, column
+    // 16 ni + r16.  Each store is one buffer_store_dword: the lane's byte offset (node, pixel, 4 qq rows)
+    // is fixed per ni and the row's part (16 mi + r rows) is a scalar offset; a 16-row block lies on one
+    // side of m0 (the launch requires m0 % 64 == 0), so its output tensor is picked per block.  Round 4's
+    // per-element 64-bit addressing (an int64 division per column, a bias load and the side select per
+    // element: ~1,800 VALU instructions per wave) cost 3-11 % of the kernel (tools/ab_gemm.py).
     const int mb0 = mt * TM + 64 * wm;
+    uint32_t vo0[4], vo1[4];  // per ni: byte offset of (node, pixel, row 4 qq) in c0 / c1
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
       const int64_t n = nbase + 64 * wn + 16 * ni + r16;
-      if (n >= a.ncols) continue;
-      const int64_t nd = n / a.P, px = n - nd * a.P;
+      const bool live = n < a.ncols;
+      const uint32_t nn = (uint32_t)(live ? n : 0);  // the launch requires ncols < 2^31
+      const uint32_t nd = nn / (uint32_t)a.P, px = nn - nd * (uint32_t)a.P;
+      // columns past the end: an offset past the buffer's 2^31 - 1 bytes, so the store is dropped
+      // (the range check covers the lane offset, not the scalar one)
+      vo0[ni] = live ? 4u * ((uint32_t)((int64_t)nd * a.c0s) + px + (uint32_t)(4 * qq * a.P)) : 0x80000000u;
+      vo1[ni] = live ? 4u * ((uint32_t)((int64_t)nd * a.c1s) + px + (uint32_t)(4 * qq * a.P)) : 0x80000000u;
+    }
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < 4; ++mi) {
+      const int mrow = mb0 + 16 * mi;  // the block's first row (wave-uniform)
+      const bool side1 = mrow >= a.m0;
+      const uint32_t srow = (uint32_t)(side1 ? mrow - a.m0 : mrow);
+      const __amdgpu_buffer_rsrc_t rc = rsrc(side1 ? a.c1 : a.c0);
+      f4 bv = {0.f, 0.f, 0.f, 0.f};
+      if (a.bias != nullptr) {
+        const float* bp = a.bias + mrow + 4 * qq;
+        bv = {bp[0], bp[1], bp[2], bp[3]};
+      }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = mb0 + 16 * mi + 4 * qq + r;
-          if (m >= a.M) continue;
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t so = 4u * (srow + (uint32_t)r) * (uint32_t)a.P;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
           float v = __fadd_rn(acc[mi][ni].hi[r], acc[mi][ni].lo[r]);
-          if (a.bias != nullptr) v = __fadd_rn(v, a.bias[m]);
-          float* dst = m < a.m0 ? a.c0 + nd * a.c0s + (int64_t)m * a.P + px
-                                : a.c1 + nd * a.c1s + (int64_t)(m - a.m0) * a.P + px;
-          *dst = v;
+          if (a.bias != nullptr) v = __fadd_rn(v, bv[r]);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, side1 ? vo1[ni] : vo0[ni], so, 0);
         }
+      }
     }
     return;
   }
@@ -469,6 +490,16 @@ hipError_t launch_w(Args a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// the 16x16x32 form's epilogue: 16-row blocks on one side of m0, 32-bit buffer offsets into c0 / c1
+bool mf16_ok(const Args& a) {
+  if (a.M % 256 != 0 || a.m0 % 64 != 0 || a.ncols >= kOffMax) return false;
+  const int64_t nodes = a.ncols / a.P;
+  const int64_t r0 = a.m0 < a.M ? a.m0 : a.M, r1 = a.M - r0;
+  const int64_t e0 = ((nodes - 1) * a.c0s + r0 * a.P) * 4;
+  const int64_t e1 = r1 > 0 ? ((nodes - 1) * a.c1s + r1 * a.P) * 4 : 0;
+  return e0 < kOffMax && e1 < kOffMax;
+}
+
 hipError_t launch(Args a, hipStream_t st) {
   if (a.K % BK != 0 || a.k0 % BK != 0 || a.M % 32 != 0 || a.P % 4 != 0) return hipErrorNotSupported;
   if ((int64_t)a.M * a.K * 6 >= kOffMax) return hipErrorNotSupported;
@@ -478,8 +509,9 @@ hipError_t launch(Args a, hipStream_t st) {
   // at every config shape (the smaller MFMA holds a higher clock under the power limit) — are lab forms
   // now (tools/lab_forms.hip).
   int v = mrp_host::tuning().gemm_split;
-  if (v < 0) v = a.M % 256 == 0 ? 7 : 2;
-  if (v == 7 && a.M % 256 == 0) return launch_w<4, gemm_nn_split_w4_mf16>(a, st);
+  const bool mf16 = mf16_ok(a);
+  if (v < 0) v = mf16 ? 7 : 2;
+  if (v == 7 && mf16) return launch_w<4, gemm_nn_split_w4_mf16>(a, st);
   return launch_w<2, gemm_nn_split_w2>(a, st);
 }
 
