@@ -418,7 +418,10 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * MFMAs); "split_nt" (split-bf16 weight gradient of mrp_compress_bwd_weight_split and
  * mrp_edge_encoder_bwd_split: -1 per shape, 3 = both operands split in the kernel on 16x16x32 MFMAs,
  * 4 = the compress weight gradient with dy split once (split_rows + gemm_nt_psa; the default where
- * C >= 1024)).  Round 4's other kernel forms are lab code (tools/lab_*.hip) since ABI 18. */
+ * C >= 1024)).  Round 4's other kernel forms are lab code (tools/lab_*.hip) since ABI 18.  Tile order
+ * of the split-bf16 GEMMs: "gemm_group" (runs of this many 256-row tiles walked m fastest, so an XCD's
+ * concurrent workgroups share row and column blocks in its L2; 4 default, 0 = all, 1..64) for the
+ * forward / data gradient, "nt_group" (the same, default 0) for the weight gradient. */
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 18 = this header: v17 without

@@ -158,10 +158,27 @@ struct Args {
   const float* bias;  // (M) or null
   int64_t ncols;      // nodes * P
   int32_t M, K, k0, m0, P, mtiles;
+  int32_t group;  // tile order (tile_of)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+// Tile t of an mtiles x ntiles grid, in runs of `group` m-tiles walked m fastest (group <= 0: all of
+// them, round 4's order).  An XCD runs ~32 consecutive tiles at once (the XCD-aware remap gives it a
+// contiguous range), and they share its L2: with group 4 that window is 4 m-tiles x 8 column tiles,
+// so the L2 misses per window are 4 row blocks of the packed operand plus 8 column blocks of the
+// streamed one — at configs[3] (8 m-tiles x 32 column tiles) 42 MB per XCD against 59 MB for 8 x 4,
+// and for its data gradient (16 m-tiles) 21 against 52 MB.
+__device__ __forceinline__ void tile_of(int t, int mtiles, int ntiles, int group, int& mt, int& nt) {
+  const int gmax = group > 0 && group < mtiles ? group : mtiles;
+  const int run = gmax * ntiles;
+  const int g = t / run, first = g * gmax;
+  const int gm = mtiles - first < gmax ? mtiles - first : gmax;
+  const int rem = t - g * run;
+  mt = first + rem % gm;
+  nt = rem / gm;
 }
 
 template <int WMW, bool MF16 = false>
@@ -175,7 +192,8 @@ __device__ __forceinline__ void gemm_nn_split_body(const Args& a) {
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-  const int mt = id % a.mtiles, nt = id / a.mtiles;
+  int mt, nt;
+  tile_of(id, a.mtiles, nwg / a.mtiles, a.group, mt, nt);
   const int64_t nbase = (int64_t)nt * TN;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -486,6 +504,7 @@ hipError_t launch_w(Args a, hipStream_t st) {
   static const hipError_t attr =
       hipFuncSetAttribute(reinterpret_cast<const void*>(K), hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
   if (attr != hipSuccess) return attr;
+  a.group = mrp_host::tuning().gemm_group;
   hipLaunchKernelGGL(K, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
   return hipGetLastError();
 }
@@ -537,6 +556,7 @@ struct NTArgs {
   int64_t ktot, kchunk;
   int32_t M, N, n0, P, mtiles, ntiles;
   const u4* ap;  // gemm_nt_psa: the pre-split image of g (split_rows), KS = ktot / 16 16-k steps per row block
+  int32_t group;  // tile order (tile_of)
 };
 
 template <int WMW>
@@ -567,7 +587,8 @@ __device__ __forceinline__ void gemm_nt_split_body(const NTArgs& a, int orig, in
   const int id = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + orig / 8;
   const int tiles = a.mtiles * a.ntiles;
   const int split = id / tiles, tid = id - split * tiles;
-  const int mt = tid % a.mtiles, nt = tid / a.mtiles;
+  int mt, nt;
+  tile_of(tid, a.mtiles, a.ntiles, a.group, mt, nt);
   const int mbase = mt * G::TM, nbase = nt * TN;
   const int64_t kbeg = (int64_t)split * a.kchunk;
   const int64_t kend = kbeg + a.kchunk < a.ktot ? kbeg + a.kchunk : a.ktot;
@@ -788,7 +809,8 @@ __device__ __forceinline__ void gemm_nt_psa_body(const NTArgs& a, int orig, int 
   const int id = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + orig / 8;
   const int tiles = a.mtiles * a.ntiles;
   const int split = id / tiles, tid = id - split * tiles;
-  const int mt = tid % a.mtiles, nt = tid / a.mtiles;
+  int mt, nt;
+  tile_of(tid, a.mtiles, a.ntiles, a.group, mt, nt);
   const int mbase = mt * G::TM, nbase = nt * TN;
   const int64_t kbeg = (int64_t)split * a.kchunk;
   const int64_t kend = kbeg + a.kchunk < a.ktot ? kbeg + a.kchunk : a.ktot;
@@ -1134,6 +1156,7 @@ hipError_t nt_run(NTArgs a, int64_t M, int64_t N, int32_t nodes, float* out, flo
   static const hipError_t attr16 = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_split_w4_mf16),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
   if (attr16 != hipSuccess) return attr16;
+  a.group = mrp_host::tuning().nt_group;
   hipLaunchKernelGGL(gemm_nt_split_w4_mf16, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ns == 1) return e;
@@ -1199,6 +1222,7 @@ hipError_t psa_gemm(NTArgs a, int64_t M, int64_t N, const u4* img, const float* 
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_psa),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
   if (attr != hipSuccess) return attr;
+  a.group = mrp_host::tuning().nt_group;
   hipLaunchKernelGGL(gemm_nt_psa, dim3((unsigned)grid), dim3(G::THREADS), G::LDS_BYTES, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -1542,6 +1566,7 @@ extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, con
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_dual_mf16),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, GN::LDS_BYTES);
   if (attr != hipSuccess) return attr;
+  a1.group = a2.group = mrp_host::tuning().nt_group;
   hipLaunchKernelGGL(gemm_nt_dual_mf16, dim3((unsigned)(grid1 + grid2)), dim3(GN::THREADS), GN::LDS_BYTES, st, a1,
                      a2, grid1);
   if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -107,6 +107,8 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"edge_allx", &t.edge_allx, 0, 1},
       {"gemm_split", &t.gemm_split, -1, 7},
       {"split_nt", &t.split_nt, -1, 4},
+      {"gemm_group", &t.gemm_group, 0, 64},
+      {"nt_group", &t.nt_group, 0, 64},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {

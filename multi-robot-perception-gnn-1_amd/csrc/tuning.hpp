@@ -43,6 +43,12 @@ struct Tuning {
   // offsets, else (and for the encoder's products) 3 (the default below C = 1024): the 32-k-stage form
   // on 16x16x32 MFMAs splitting both operands
   int split_nt = -1;
+  // split-bf16 GEMMs' tile order (compress_split.hip tile_of): runs of this many 256-row tiles, m
+  // fastest (0: all, round 4's order).  Forward / data gradient 4 (configs[3] 1.4-1.8 % faster, the
+  // others flat; tools/ab_gemm.py knob:gemm_group=0,4); weight gradient 0 (4 measured 1.6-2.7 % slower
+  // at configs[2] and [3])
+  int gemm_group = 4;
+  int nt_group = 0;
 };
 Tuning& tuning();
 

@@ -4,7 +4,8 @@ library (B, tools/build_variant_lib.py) in one process, alternated per round, HI
 (bench.time_launches) at the configs[1..4] layer shapes and the headline layer shape: forward, data
 gradient, weight gradient, and the three back to back (one graph: the order a training step runs
 them, where the chip's power limit sets the clock).
-usage: python tools/ab_gemm.py tools/bin/<variant>.so [iters] [rounds] [shapes, e.g. cfg1,cfg3]"""
+usage: python tools/ab_gemm.py tools/bin/<variant>.so [iters] [rounds] [shapes, e.g. cfg1,cfg3]
+       python tools/ab_gemm.py knob:<name>=<a>,<b> ...   (the product library at two knob values)"""
 import ctypes
 import os
 import sys
@@ -22,8 +23,14 @@ iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 only = sys.argv[4].split(",") if len(sys.argv) > 4 else None
 lib_a = _lib.load_library()
-lib_b = ctypes.CDLL(os.path.abspath(path_b))
-_lib._declare(lib_b)
+if path_b.startswith("knob:"):
+    knob, vals = path_b[5:].split("=")
+    va, vb = (int(v) for v in vals.split(","))
+    lib_b = lib_a
+else:
+    knob = None
+    lib_b = ctypes.CDLL(os.path.abspath(path_b))
+    _lib._declare(lib_b)
 dev = torch.device("cuda:0")
 cm = mrp.compress
 cm.set_compress_path("split")
@@ -47,12 +54,16 @@ for name, n, C, H in SHAPES:
     for _ in range(rounds):
         for lab, lib in (("A", lib_a), ("B", lib_b)):
             _lib._lib = lib
+            if knob:
+                assert lib.mrp_tuning_set(knob.encode(), va if lab == "A" else vb) == 0
             for k, f in ops.items():
                 res.setdefault((lab, k), []).append(bench.time_launches([f], iters, dev))
                 if k != "step" and (lab, k) not in outs:
                     o = f()
                     outs[(lab, k)] = [t.clone() for t in (o if isinstance(o, tuple) else (o,)) if t is not None]
     _lib._lib = lib_a
+    if knob:
+        lib_a.mrp_tuning_set(b"reset", 0)
     line = [f"{name} n={n} C={C} {H}x{H}"]
     for k in ops:
         ta, tb = min(res[("A", k)]), min(res[("B", k)])
