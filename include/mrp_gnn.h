@@ -345,7 +345,10 @@ int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const floa
  *                                      on one stream: dz^T; dh^T and dW2 as ONE launch of both split-K
  *                                      products; a reduction that sums their partial tiles, applies the
  *                                      ReLU mask and forms dW1 / db1 (dh^T never written).  dw1, db1,
- *                                      dw2, db2 all required (no dpose);
+ *                                      dw2, db2 all required (no dpose); w2T_packed: NULL, or W2^T's
+ *                                      packed split image (mrp_compress_split_pack(w2, C, 1, C, 2C), 16-byte
+ *                                      aligned), which the dh^T product then reads instead of splitting
+ *                                      w2T in every workgroup (same products, same order: bit-identical);
  *                                      workspace: _fused_workspace(E, C) bytes
  * Requirements of _bwd_split and _bwd_fused (else hipErrorNotSupported): E % 32 == 0, C % 32 == 0,
  * 16-byte aligned operands.  All sums in a fixed order: deterministic.
@@ -359,9 +362,9 @@ int mrp_edge_encoder_bwd_split(const float* dz, const float* dzT, const float* w
                                int32_t num_edges, int32_t C, float* dhT, float* dw2, float* db2, void* workspace,
                                int64_t workspace_bytes, void* stream);
 int64_t mrp_edge_encoder_bwd_fused_workspace(int32_t num_edges, int32_t C);
-int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, const float* hT, const float* pose,
-                               int32_t num_edges, int32_t C, float* dw1, float* db1, float* dw2, float* db2,
-                               void* workspace, int64_t workspace_bytes, void* stream);
+int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, const void* w2T_packed, const float* hT,
+                               const float* pose, int32_t num_edges, int32_t C, float* dw1, float* db1, float* dw2,
+                               float* db2, void* workspace, int64_t workspace_bytes, void* stream);
 int64_t mrp_edge_encoder_bwd_t_workspace(int32_t num_edges, int32_t C);
 int mrp_edge_encoder_bwd_t(const float* dhT, int64_t dhT_stride, const float* hT, int64_t hT_stride,
                            const float* pose, int32_t num_edges, int32_t C, float* dw1, float* db1, void* workspace,
@@ -421,10 +424,12 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * C >= 1024)).  Round 4's other kernel forms are lab code (tools/lab_*.hip) since ABI 18.  Tile order
  * of the split-bf16 GEMMs: "gemm_group" (runs of this many 256-row tiles walked m fastest, so an XCD's
  * concurrent workgroups share row and column blocks in its L2; 4 default, 0 = all, 1..64) for the
- * forward / data gradient, "nt_group" (the same, default 0) for the weight gradient. */
+ * forward / data gradient, "nt_group" (the same, default 0) for the weight gradient; "enc_bwd_psa"
+ * (1 default: mrp_edge_encoder_bwd_fused reads w2T_packed when given; 0: splits w2T in the kernel). */
 int mrp_tuning_set(const char* name, int32_t value);
 
-/* Library identification: ABI version (incremented on signature changes; 18 = this header: v17 without
+/* Library identification: ABI version (incremented on signature changes; 19 = this header: v18 with
+ * mrp_edge_encoder_bwd_fused taking W2^T's packed image (w2T_packed); 18: v17 without
  * mrp_edge_encoder_fwd (the fp32 one-launch encoder, superseded by mrp_edge_encoder_fwd_split) and
  * with fewer tuning knobs (only those that select kernels the library builds); 17: v16 plus
  * the split-bf16 training path of the edge encoder (mrp_edge_encoder_fwd_split_train, _bwd_prep,

@@ -56,7 +56,7 @@ EXPORTED_SYMBOLS = (
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 18
+ABI_VERSION = 19
 MAX_NODES = 16
 
 HIP_ERROR_NOT_SUPPORTED = 801  # hipErrorNotSupported: a fused path declines this shape
@@ -153,7 +153,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_edge_encoder_bwd_split.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_fused_workspace.argtypes = [_I32, _I32]
     lib.mrp_edge_encoder_bwd_fused_workspace.restype = ctypes.c_int64
-    lib.mrp_edge_encoder_bwd_fused.argtypes = [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _I64, _P]
+    lib.mrp_edge_encoder_bwd_fused.argtypes = [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _I64, _P]
     lib.mrp_edge_encoder_bwd_fused.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_t_workspace.argtypes = [_I32, _I32]
     lib.mrp_edge_encoder_bwd_t_workspace.restype = ctypes.c_int64

@@ -987,6 +987,15 @@ __device__ __forceinline__ void gemm_nt_psa_body(const NTArgs& a, int orig, int 
 
 __global__ void __launch_bounds__(512, 1) gemm_nt_psa(NTArgs a) { gemm_nt_psa_body(a, blockIdx.x, gridDim.x); }
 
+// the same with the first product's A operand pre-split (gemm_nt_psa_body: the edge encoder's W2^T,
+// packed once per weight version) — the split body re-split it once per column tile and call
+__global__ void __launch_bounds__(512, 1) gemm_nt_dual_psa1(NTArgs a1, NTArgs a2, int grid1) {
+  if ((int)blockIdx.x < grid1)
+    gemm_nt_psa_body(a1, blockIdx.x, grid1);
+  else
+    gemm_nt_split_body<4>(a2, blockIdx.x - grid1, gridDim.x - grid1);
+}
+
 // two independent NT products in one launch (the edge encoder's backward), on the default (16x16x32)
 // form: workgroups [0, grid1) run a1, the rest a2, each product with its own XCD-aware tile order
 __global__ void __launch_bounds__(512, 1) gemm_nt_dual_mf16(NTArgs a1, NTArgs a2, int grid1) {
@@ -1502,9 +1511,10 @@ extern "C" int64_t mrp_edge_encoder_bwd_fused_workspace(int32_t num_edges, int32
   return mrp_cs::enc_plan(num_edges, C).bytes;
 }
 
-extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, const float* hT, const float* pose,
-                                          int32_t num_edges, int32_t C, float* dw1, float* db1, float* dw2,
-                                          float* db2, void* workspace, int64_t workspace_bytes, void* stream) {
+extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, const void* w2T_packed, const float* hT,
+                                          const float* pose, int32_t num_edges, int32_t C, float* dw1, float* db1,
+                                          float* dw2, float* db2, void* workspace, int64_t workspace_bytes,
+                                          void* stream) {
   using namespace mrp_cs;
   if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
   if (C == 0) return hipSuccess;
@@ -1544,6 +1554,11 @@ extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, con
   a1.N = (int32_t)E;
   a1.mtiles = (int32_t)((C + NTGeo<4>::TM - 1) / NTGeo<4>::TM);
   a1.ntiles = (int32_t)((E + TN - 1) / TN);
+  // W2^T's packed image (mrp_compress_split_pack(w2, C, 1, C, 2C)): the first product reads its A by
+  // LDS-DMA instead of splitting W2^T in every workgroup (knob enc_bwd_psa 0: the split form)
+  const bool psa1 = w2T_packed != nullptr && aligned16(w2T_packed) && mrp_host::tuning().enc_bwd_psa != 0 &&
+                    (int64_t)C * C2 * 6 < kOffMax;
+  a1.ap = psa1 ? static_cast<const u4*>(w2T_packed) : nullptr;
   NTArgs a2 = {};  // dW2 (2C x C) = dz^T (2C x E) . h: rows j, k = e; row sums = db2
   a2.g = dzT;
   a2.gs = C2 * E;
@@ -1566,9 +1581,16 @@ extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, con
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_dual_mf16),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, GN::LDS_BYTES);
   if (attr != hipSuccess) return attr;
+  static const hipError_t attr_p = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_dual_psa1),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, GN::LDS_BYTES);
+  if (attr_p != hipSuccess) return attr_p;
   a1.group = a2.group = mrp_host::tuning().nt_group;
-  hipLaunchKernelGGL(gemm_nt_dual_mf16, dim3((unsigned)(grid1 + grid2)), dim3(GN::THREADS), GN::LDS_BYTES, st, a1,
-                     a2, grid1);
+  if (psa1)
+    hipLaunchKernelGGL(gemm_nt_dual_psa1, dim3((unsigned)(grid1 + grid2)), dim3(GN::THREADS), GN::LDS_BYTES, st, a1,
+                       a2, grid1);
+  else
+    hipLaunchKernelGGL(gemm_nt_dual_mf16, dim3((unsigned)(grid1 + grid2)), dim3(GN::THREADS), GN::LDS_BYTES, st, a1,
+                       a2, grid1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int nb1 = C;
   const int64_t nb2 = (C2 * C / 4 + 255) / 256;  // >= 2C / 256 blocks: db2 rides along

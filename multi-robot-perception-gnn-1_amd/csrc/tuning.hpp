@@ -49,6 +49,9 @@ struct Tuning {
   // at configs[2] and [3])
   int gemm_group = 4;
   int nt_group = 0;
+  // mrp_edge_encoder_bwd_fused: the dh^T product's W2^T from its packed image when one is given (1), or
+  // split in every workgroup (0)
+  int enc_bwd_psa = 1;
 };
 Tuning& tuning();
 

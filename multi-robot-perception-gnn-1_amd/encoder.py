@@ -75,6 +75,7 @@ _packed = weakref.WeakKeyDictionary()
 def clear_packed_weights() -> None:
     _packed.clear()
     _w2t_cache.clear()
+    _w2t_img_cache.clear()
 
 
 def packed_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> torch.Tensor:
@@ -238,6 +239,7 @@ PATH_COUNTS = collections.Counter()
 
 
 _w2t_cache = weakref.WeakKeyDictionary()
+_w2t_img_cache = weakref.WeakKeyDictionary()
 
 #: the single-stream fused encoder backward (``mrp_edge_encoder_bwd_fused``) when every parameter
 #: gradient and no pose gradient is wanted; False: the two-stream form (A/B comparisons)
@@ -260,6 +262,27 @@ def transposed_w2(l2: torch.nn.Linear) -> torch.Tensor:
     t = w2.detach().float().t().contiguous()
     _w2t_cache[l2] = (key, t)
     return t
+
+
+def packed_w2t(l2: torch.nn.Linear) -> torch.Tensor:
+    """W2^T's packed split-bf16 image (``mrp_compress_split_pack(w2, C, 1, C, 2C)``) — the dh^T product's
+    row operand in ``mrp_edge_encoder_bwd_fused`` — cached per weight version like :func:`transposed_w2`."""
+    w2 = l2.weight
+    key = (w2.data_ptr(), w2._version, w2.device.index)
+    hit = _w2t_img_cache.get(l2)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    C = w2.shape[1]
+    lib = _lib.load_library()
+    nbytes = int(lib.mrp_compress_split_pack_bytes(C, 2 * C))
+    img = torch.empty((nbytes + 3) // 4, device=w2.device, dtype=torch.float32)
+    w2c = w2.detach().contiguous().float()
+    with torch.cuda.device(w2.device):
+        _lib.check(lib.mrp_compress_split_pack(_ptr(w2c), C, 1, C, 2 * C, _ptr(img),
+                                               ctypes.c_void_p(torch.cuda.current_stream(w2.device).cuda_stream)),
+                   "mrp_compress_split_pack")
+    _w2t_img_cache[l2] = (key, img)
+    return img
 
 
 def image_supported(C: int) -> bool:
@@ -288,7 +311,7 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
       gradient all-reducer's buckets when one holds the parameters (``dist.grad_out_like``)."""
 
     @staticmethod
-    def forward(ctx, pose, w1, b1, w2, b2, img, w2t):
+    def forward(ctx, pose, w1, b1, w2, b2, img, w2t, w2t_img=None):
         E, C = pose.shape[0], w1.shape[0]
         pose = pose.detach().contiguous().float()
         b2c = b2.detach().contiguous().float() if b2 is not None else None
@@ -300,6 +323,7 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
                 _ptr(pose), _ptr(img), _ptr(b2c) if b2c is not None else None, E, C, _ptr(z), _ptr(hT), E,
                 ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
         ctx.save_for_backward(pose, w1, b1, w2, b2, hT, w2t)
+        ctx.w2t_img = w2t_img
         return z
 
     @staticmethod
@@ -323,10 +347,12 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
             dw2, db2 = _grad_out(w2, (2 * C, C), dev), _grad_out(b2, (2 * C,), dev)
             wsf = torch.empty((int(lib.mrp_edge_encoder_bwd_fused_workspace(E, C)) + 3) // 4, device=dev)
             with torch.cuda.device(dev):
+                w2t_img = ctx.w2t_img
                 _lib.check(lib.mrp_edge_encoder_bwd_fused(
-                    _ptr(dz), _ptr(w2t), _ptr(hT), _ptr(pose), E, C, _ptr(dw1), _ptr(db1), _ptr(dw2), _ptr(db2),
+                    _ptr(dz), _ptr(w2t), _ptr(w2t_img) if w2t_img is not None else None, _ptr(hT), _ptr(pose), E, C,
+                    _ptr(dw1), _ptr(db1), _ptr(dw2), _ptr(db2),
                     _ptr(wsf), wsf.numel() * 4, ctypes.c_void_p(cur.cuda_stream)), "mrp_edge_encoder_bwd_fused")
-            return None, dw1, db1, dw2, db2, None, None
+            return None, dw1, db1, dw2, db2, None, None, None
         dw2 = db2 = side = None
         with torch.cuda.device(dev):
             if need[3] or need[4]:  # dz^T, then dW2 = dz^T h with db2 as its row sums, on the side stream
@@ -362,7 +388,7 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
             if side is not None:
                 cur.wait_stream(side)
         dpose = (dhT * (hT > 0)).t().mm(w1.float()) if need[0] else None
-        return dpose, dw1, db1, dw2 if need[3] else None, db2, None, None
+        return dpose, dw1, db1, dw2 if need[3] else None, db2, None, None, None
 
 
 def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Tensor:
@@ -383,6 +409,6 @@ def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Te
             and tuple(l1.weight.shape) == (C, 9) and tuple(l2.weight.shape) == (2 * C, C):
         PATH_COUNTS["split_train"] += 1
         return EdgeEncoderSplitFunction.apply(pose, l1.weight, l1.bias, l2.weight, l2.bias,
-                                              packed_weights(l1, l2), transposed_w2(l2))
+                                              packed_weights(l1, l2), transposed_w2(l2), packed_w2t(l2))
     PATH_COUNTS["autograd"] += 1
     return EdgeEncoderFunction.apply(*params)

@@ -157,10 +157,11 @@ def test_split_encoder_training_validation_without_launch():
     ws = lib.mrp_edge_encoder_bwd_fused_workspace(1792, 512)
     assert ws >= (2 * 512 * 1792 + 7 * 512 * 10) * 4  # at least dz^T and the dW1/db1 partials
     assert lib.mrp_edge_encoder_bwd_fused_workspace(100, 512) == 0
-    assert lib.mrp_edge_encoder_bwd_fused(None, None, None, None, 96, 64, None, None, None, None, None, 0, None) == \
+    assert lib.mrp_edge_encoder_bwd_fused(None, None, None, None, None, 96, 64, None, None, None, None, None, 0,
+                                          None) == HIP_INVALID_VALUE
+    assert lib.mrp_edge_encoder_bwd_fused(16, 16, None, 16, 16, 100, 64, 16, 16, 16, 16, None, 0, None) == NS
+    assert lib.mrp_edge_encoder_bwd_fused(16, 16, 16, 16, 16, 96, 64, 16, 16, 16, 16, None, 0, None) == \
         HIP_INVALID_VALUE
-    assert lib.mrp_edge_encoder_bwd_fused(16, 16, 16, 16, 100, 64, 16, 16, 16, 16, None, 0, None) == NS
-    assert lib.mrp_edge_encoder_bwd_fused(16, 16, 16, 16, 96, 64, 16, 16, 16, 16, None, 0, None) == HIP_INVALID_VALUE
 
 
 def test_split_compress_validation_without_launch():
@@ -187,7 +188,7 @@ def test_tuning_knobs_documented_in_the_header():
     try:
         for name, lo, hi in (("bwd_regular_mfma", 0, 1), ("bwd_complete_mfma", 0, 1), ("bwd_mfma_cpw", 1, 2),
                              ("bwd_pre2", 0, 2), ("fwd_regular_split", 0, 1), ("bwd_fused_cap", 1, 64),
-                             ("gemm_group", 0, 64), ("nt_group", 0, 64)):
+                             ("gemm_group", 0, 64), ("nt_group", 0, 64), ("enc_bwd_psa", 0, 1)):
             assert name.encode() in open(os.path.join(ROOT, "include", "mrp_gnn.h"), "rb").read() or \
                 name.startswith("bwd_fused")
             assert lib.mrp_tuning_set(name.encode(), lo) == 0

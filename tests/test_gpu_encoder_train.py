@@ -124,3 +124,25 @@ def test_split_training_encoder_property(cuda_device, e32, c32, form):
         _check_training_encoder(cuda_device, 32 * e32, 32 * c32, pose_grad=form == "pose_grad")
     finally:
         m.encoder.set_fused_backward(True)
+
+
+@pytest.mark.parametrize("E,C", [(1792, 512), (448, 2048), (96, 64)])
+def test_fused_backward_w2t_image_bit_identical(cuda_device, E, C):
+    """The fused backward's dh^T product reading W2^T's packed image (the default) and splitting W2^T in
+    the kernel (knob enc_bwd_psa 0) form the same products in the same order: bit-identical gradients."""
+    torch.manual_seed(E + C)
+    enc = m.edge_encoder([C, C]).to(cuda_device)
+    pose = (torch.randn(E, 9) * 8).to(cuda_device)
+    gz = torch.randn(E, 2 * C, device=cuda_device)
+    lib = m.load_library()
+    grads = []
+    try:
+        for v in (1, 0):
+            assert lib.mrp_tuning_set(b"enc_bwd_psa", v) == 0
+            enc.zero_grad(set_to_none=True)
+            m.encoder.edge_logits(enc.layers, pose).backward(gz)
+            grads.append([p.grad.clone() for p in enc.parameters()])
+    finally:
+        lib.mrp_tuning_set(b"reset", 0)
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
