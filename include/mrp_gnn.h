@@ -348,7 +348,9 @@ int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const floa
  *                                      dw2, db2 all required (no dpose); w2T_packed: NULL, or W2^T's
  *                                      packed split image (mrp_compress_split_pack(w2, C, 1, C, 2C), 16-byte
  *                                      aligned), which the dh^T product then reads instead of splitting
- *                                      w2T in every workgroup (same products, same order: bit-identical);
+ *                                      w2T in every workgroup, and dz^T is then written as a packed image
+ *                                      for the dW2 product too (same products, same order: dW1, db1 and
+ *                                      dW2 bit-identical to the split form; db2 summed per 64-edge block);
  *                                      workspace: _fused_workspace(E, C) bytes
  * Requirements of _bwd_split and _bwd_fused (else hipErrorNotSupported): E % 32 == 0, C % 32 == 0,
  * 16-byte aligned operands.  All sums in a fixed order: deterministic.
@@ -425,7 +427,8 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * of the split-bf16 GEMMs: "gemm_group" (runs of this many 256-row tiles walked m fastest, so an XCD's
  * concurrent workgroups share row and column blocks in its L2; 4 default, 0 = all, 1..64) for the
  * forward / data gradient, "nt_group" (the same, default 0) for the weight gradient; "enc_bwd_psa"
- * (1 default: mrp_edge_encoder_bwd_fused reads w2T_packed when given; 0: splits w2T in the kernel). */
+ * (mrp_edge_encoder_bwd_fused given w2T_packed: 2 default = both products read their A operand
+ * pre-split, dz^T written as a packed image; 1 = only W2^T's image; 0 = both split in the kernel). */
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 19 = this header: v18 with

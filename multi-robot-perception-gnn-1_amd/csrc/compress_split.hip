@@ -1371,6 +1371,64 @@ namespace mrp_cs {
 
 constexpr int kNin = 9;
 
+// dz (E x N2, row-major) -> the packed split image of dz^T (N2 x E, k = the edges; `pack`'s layout, the
+// dW2 product's A operand, read by LDS-DMA) and db2's partials csum[eb][j] = sum of dz[e][j] over the
+// 64-edge block eb in edge order (summed over the blocks in order by encoder_bwd_reduce).  64 x 64 tile
+// through LDS as dz_transpose; lane -> (row j0 + (u & 63), edges 8 (u >> 6) ..): a wave's 32-row halves
+// store 512 contiguous bytes per part.  E % 16 == 0.
+__global__ void __launch_bounds__(256) dzT_pack(const float* __restrict__ dz, int E, int N2, u4* __restrict__ img,
+                                                float* __restrict__ csum) {
+  __shared__ float tile[64][65];
+  const int j0 = blockIdx.x * 64, e0 = blockIdx.y * 64;
+  const int c4 = threadIdx.x & 15, r0 = threadIdx.x >> 4;
+  f4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = e0 + r0 + 16 * i, j = j0 + 4 * c4;
+    v[i] = (e < E && j < N2) ? *reinterpret_cast<const f4*>(dz + (int64_t)e * N2 + j) : f4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tile[r0 + 16 * i][4 * c4 + q] = v[i][q];
+  __syncthreads();
+  if (threadIdx.x < 64 && j0 + (int)threadIdx.x < N2) {
+    float sum = 0.f;
+    for (int e = 0; e < 64; ++e) sum += tile[e][threadIdx.x];
+    csum[(int64_t)blockIdx.y * N2 + j0 + threadIdx.x] = sum;
+  }
+  const int64_t KS = E / 16;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int u = threadIdx.x + 256 * i;
+    const int jl = u & 63, g8 = u >> 6;
+    const int j = j0 + jl, e = e0 + 8 * g8;
+    if (j >= N2 || e >= E) continue;
+    u4 p0, p1, p2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f2 x;
+      x.x = tile[8 * g8 + 2 * q][jl];
+      x.y = tile[8 * g8 + 2 * q + 1][jl];
+      uint32_t a0, a1, a2;
+      split2(x, a0, a1, a2);
+      p0[q] = a0, p1[q] = a1, p2[q] = a2;
+    }
+    const int64_t base = (((int64_t)(j >> 5) * KS + (e >> 4)) * 3) * 64 + (j & 31) + 32 * ((e >> 3) & 1);
+    img[base] = p0;
+    img[base + 64] = p1;
+    img[base + 128] = p2;
+  }
+}
+
+// both products with a pre-split A: W2^T's packed image and dz^T's (dzT_pack)
+__global__ void __launch_bounds__(512, 1) gemm_nt_dual_psa2(NTArgs a1, NTArgs a2, int grid1) {
+  if ((int)blockIdx.x < grid1)
+    gemm_nt_psa_body(a1, blockIdx.x, grid1);
+  else
+    gemm_nt_psa_body(a2, blockIdx.x - grid1, gridDim.x - grid1);
+}
+
 struct EncPlan {
   int s1, s2;
   int64_t kc1, kc2;
@@ -1406,13 +1464,14 @@ EncPlan enc_plan(int64_t E, int64_t C) {
   auto al = [](int64_t v) { return (v + 63) / 64 * 64; };  // 256-byte segments
   int64_t o = 0;
   pl.off_dzT = o;
-  o += al(C2 * E);
+  o += al(C2 * E * 3 / 2);  // dz^T in fp32, or its packed split image (6 bytes per element)
   pl.off_p1 = o;
   o += al((int64_t)pl.s1 * C * E);
   pl.off_p2 = o;
   o += al((int64_t)pl.s2 * C2 * C);
   pl.off_p2b = o;
-  o += al((int64_t)pl.s2 * C2);
+  const int64_t nb2 = (int64_t)pl.s2 > (E + 63) / 64 ? pl.s2 : (E + 63) / 64;  // db2 partials: splits or edge blocks
+  o += al(nb2 * C2);
   pl.bytes = o * 4;
   return pl;
 }
@@ -1424,7 +1483,7 @@ __global__ void __launch_bounds__(256) encoder_bwd_reduce(const float* __restric
                                                           int E, int C, float* __restrict__ dw1,
                                                           float* __restrict__ db1, int nb1,
                                                           const f4* __restrict__ p2, const float* __restrict__ p2b,
-                                                          int s2, f4* __restrict__ dw2, float* __restrict__ db2) {
+                                                          int s2, int s2b, f4* __restrict__ dw2, float* __restrict__ db2) {
   if ((int)blockIdx.x < nb1) {
     // one workgroup per hidden unit u: wave w's lanes walk edges 64 w + lane + 256 k, summing the dh^T
     // partials in split order, masking by the ReLU and accumulating d pose^T and d in registers; a
@@ -1499,7 +1558,7 @@ __global__ void __launch_bounds__(256) encoder_bwd_reduce(const float* __restric
   const int64_t m = (int64_t)b * 256 + threadIdx.x;
   if (m < 2 * C) {
     float v = p2b[m];
-    for (int sp = 1; sp < s2; ++sp) v += p2b[(int64_t)sp * 2 * C + m];
+    for (int sp = 1; sp < s2b; ++sp) v += p2b[(int64_t)sp * 2 * C + m];
     db2[m] = v;
   }
 }
@@ -1535,7 +1594,21 @@ extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, con
   if (workspace == nullptr || !aligned16(workspace) || workspace_bytes < pl.bytes) return hipErrorInvalidValue;
   float* ws = static_cast<float*>(workspace);
   float* dzT = ws + pl.off_dzT;
-  hipError_t e = (hipError_t)mrp_edge_encoder_bwd_prep(dz, num_edges, C, dzT, E, stream);
+  // W2^T's packed image (mrp_compress_split_pack(w2, C, 1, C, 2C)): the dh^T product reads its A by
+  // LDS-DMA instead of splitting W2^T in every workgroup; and (enc_bwd_psa 2, the default) dz^T is
+  // written as a packed image too (dzT_pack, with db2's partials), so the dW2 product reads both its
+  // operands' A side pre-split.  enc_bwd_psa 0: both split in the kernel, 1: only W2^T pre-split.
+  const int mode = mrp_host::tuning().enc_bwd_psa;
+  const bool psa1 = w2T_packed != nullptr && aligned16(w2T_packed) && mode >= 1 && (int64_t)C * C2 * 6 < kOffMax;
+  const bool psa2 = psa1 && mode >= 2 && C2 * E * 6 < kOffMax;
+  hipError_t e;
+  if (psa2) {
+    hipLaunchKernelGGL(dzT_pack, dim3((unsigned)((C2 + 63) / 64), (unsigned)((E + 63) / 64)), dim3(256), 0, st, dz,
+                       num_edges, (int)C2, reinterpret_cast<u4*>(dzT), ws + pl.off_p2b);
+    e = hipGetLastError();
+  } else {
+    e = (hipError_t)mrp_edge_encoder_bwd_prep(dz, num_edges, C, dzT, E, stream);
+  }
   if (e != hipSuccess) return e;
   NTArgs a1 = {};  // dh^T (C x E) = W2^T (C x 2C) . dz^T: rows u, k = j
   a1.g = w2T;
@@ -1554,10 +1627,6 @@ extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, con
   a1.N = (int32_t)E;
   a1.mtiles = (int32_t)((C + NTGeo<4>::TM - 1) / NTGeo<4>::TM);
   a1.ntiles = (int32_t)((E + TN - 1) / TN);
-  // W2^T's packed image (mrp_compress_split_pack(w2, C, 1, C, 2C)): the first product reads its A by
-  // LDS-DMA instead of splitting W2^T in every workgroup (knob enc_bwd_psa 0: the split form)
-  const bool psa1 = w2T_packed != nullptr && aligned16(w2T_packed) && mrp_host::tuning().enc_bwd_psa != 0 &&
-                    (int64_t)C * C2 * 6 < kOffMax;
   a1.ap = psa1 ? static_cast<const u4*>(w2T_packed) : nullptr;
   NTArgs a2 = {};  // dW2 (2C x C) = dz^T (2C x E) . h: rows j, k = e; row sums = db2
   a2.g = dzT;
@@ -1569,7 +1638,8 @@ extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, con
   a2.n0 = C;
   a2.P = (int32_t)E;
   a2.out = ws + pl.off_p2;
-  a2.outb = ws + pl.off_p2b;
+  a2.outb = psa2 ? nullptr : ws + pl.off_p2b;  // psa2: db2's partials came from dzT_pack
+  a2.ap = psa2 ? reinterpret_cast<const u4*>(dzT) : nullptr;
   a2.ktot = E;
   a2.kchunk = pl.kc2;
   a2.M = (int32_t)C2;
@@ -1584,8 +1654,14 @@ extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, con
   static const hipError_t attr_p = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_dual_psa1),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, GN::LDS_BYTES);
   if (attr_p != hipSuccess) return attr_p;
+  static const hipError_t attr_p2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_dual_psa2),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, GN::LDS_BYTES);
+  if (attr_p2 != hipSuccess) return attr_p2;
   a1.group = a2.group = mrp_host::tuning().nt_group;
-  if (psa1)
+  if (psa2)
+    hipLaunchKernelGGL(gemm_nt_dual_psa2, dim3((unsigned)(grid1 + grid2)), dim3(GN::THREADS), GN::LDS_BYTES, st, a1,
+                       a2, grid1);
+  else if (psa1)
     hipLaunchKernelGGL(gemm_nt_dual_psa1, dim3((unsigned)(grid1 + grid2)), dim3(GN::THREADS), GN::LDS_BYTES, st, a1,
                        a2, grid1);
   else
@@ -1596,6 +1672,6 @@ extern "C" int mrp_edge_encoder_bwd_fused(const float* dz, const float* w2T, con
   const int64_t nb2 = (C2 * C / 4 + 255) / 256;  // >= 2C / 256 blocks: db2 rides along
   hipLaunchKernelGGL(encoder_bwd_reduce, dim3((unsigned)(nb1 + nb2)), dim3(256), 0, st, ws + pl.off_p1, pl.s1, hT, pose,
                      num_edges, C, dw1, db1, nb1, reinterpret_cast<const f4*>(ws + pl.off_p2), ws + pl.off_p2b,
-                     pl.s2, reinterpret_cast<f4*>(dw2), db2);
+                     pl.s2, psa2 ? (int)((E + 63) / 64) : pl.s2, reinterpret_cast<f4*>(dw2), db2);
   return hipGetLastError();
 }

@@ -109,7 +109,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"split_nt", &t.split_nt, -1, 4},
       {"gemm_group", &t.gemm_group, 0, 64},
       {"nt_group", &t.nt_group, 0, 64},
-      {"enc_bwd_psa", &t.enc_bwd_psa, 0, 1},
+      {"enc_bwd_psa", &t.enc_bwd_psa, 0, 2},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {

@@ -49,9 +49,9 @@ struct Tuning {
   // at configs[2] and [3])
   int gemm_group = 4;
   int nt_group = 0;
-  // mrp_edge_encoder_bwd_fused: the dh^T product's W2^T from its packed image when one is given (1), or
-  // split in every workgroup (0)
-  int enc_bwd_psa = 1;
+  // mrp_edge_encoder_bwd_fused, given W2^T's packed image: 2 = both products read their A operand
+  // pre-split (W2^T's image; dz^T written as an image by dzT_pack), 1 = only W2^T's, 0 = neither
+  int enc_bwd_psa = 2;
 };
 Tuning& tuning();
 
