@@ -410,6 +410,10 @@ def config_record(cid, world, rank, device, args):
     def train():
         for p in net.parameters():
             p.grad = None
+        # the input stands in for the backbone's output (not a leaf in the reference's training,
+        # dgl/training.py:192-209): its gradient is computed and written every step, never added to
+        # the previous step's (which would time an extra N C H W accumulation per step)
+        xr.grad = None
         if reducer is not None:
             reducer.arm()
         net(g, xr).backward(gy)
