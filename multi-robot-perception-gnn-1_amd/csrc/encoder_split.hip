@@ -402,14 +402,20 @@ hipError_t launch_fwd2(int nwv, const FwdArgs& a, hipStream_t st) {
 }
 
 // the form per shape (mrp_tuning_set "edge_split_v": 3 = 8 waves, 1 = 4 waves per workgroup): 8 waves
-// when that gives at least 192 workgroups, else 4.  Per shape (tools/enc_lab.cpp, us, round 3's per-wave
+// when that gives one round of 192..256 workgroups, else 4 (round 5; round 4: at least 192).  Per shape (tools/enc_lab.cpp, us, round 3's per-wave
 // hidden layer / (1, 4) / (1, 8)): E=1792 C=512 18.7 / 18.5 / 16.7, E=896 C=512 13.3 / 12.6 / 15.3,
 // E=1792 C=1280 99.7 / 91.3 / 94.7, E=448 C=2048 55.4 / 60.5 / 52.6, E=512 C=1024 21.0 / 21.2 / 26.4;
 // two column blocks per wave slower everywhere.  Round 3's per-wave form (edge_split_v 0) and the
 // two-column-block forms are no longer built (their source: tools/lab_encoder_r3.hip).
+// Round 5 (tools/ab_encoder_waves.py, HIP-graph timed, us for 4 / 8 waves): E=1792 C=512 19.1 / 17.7,
+// E=896 C=512 13.1 / 16.0, E=1792 C=1280 88.5 / 92.4, E=448 C=2048 57.3 / 51.6, E=512 C=1024 20.4 / 25.1:
+// 8 waves only where their grid is one round of 192..256 workgroups (one per CU)
 int fwd2_waves(int32_t num_edges, int32_t C) {
   int v = mrp_host::tuning().edge_split_v;
-  if (v < 0) v = ((int64_t)(num_edges + 31) / 32) * (2 * (int64_t)C / 256) >= 192 ? 3 : 1;
+  if (v < 0) {
+    const int64_t grid8 = ((int64_t)(num_edges + 31) / 32) * (2 * (int64_t)C / 256);
+    v = grid8 >= 192 && grid8 <= 256 ? 3 : 1;
+  }
   return v == 3 ? 8 : 4;
 }
 
