@@ -428,7 +428,8 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * concurrent workgroups share row and column blocks in its L2; 4 default, 0 = all, 1..64) for the
  * forward / data gradient, "nt_group" (the same, default 0) for the weight gradient; "enc_bwd_psa"
  * (mrp_edge_encoder_bwd_fused given w2T_packed: 2 default = both products read their A operand
- * pre-split, dz^T written as a packed image; 1 = only W2^T's image; 0 = both split in the kernel). */
+ * pre-split, dz^T written as a packed image; 1 = only W2^T's image; 0 = both split in the kernel);
+ * "enc_s1" / "enc_s2" (its two products' split-K counts, 0 = the planner's). */
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 19 = this header: v18 with

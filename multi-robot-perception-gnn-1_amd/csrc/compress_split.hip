@@ -34,6 +34,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "mrp_gnn.h"
 #include "tuning.hpp"
 
@@ -1442,25 +1448,57 @@ EncPlan enc_plan(int64_t E, int64_t C) {
   pl.t1 = (int)(((C + NTGeo<4>::TM - 1) / NTGeo<4>::TM) * ((E + TN - 1) / TN));       // dh^T: M = C, N = E
   pl.t2 = (int)(((C2 + NTGeo<4>::TM - 1) / NTGeo<4>::TM) * ((C + TN - 1) / TN));      // dW2: M = 2C, N = C
   const int64_t st1 = C2 / BK, st2 = E / BK;                                // 32-k split granules
-  double best = 1e300;
-  pl.s1 = pl.s2 = 1;
-  for (int a = 1; a <= 64; ++a)
-    for (int b = 1; b <= 64; ++b) {
-      const int64_t p1 = (st1 + a - 1) / a, p2 = (st2 + b - 1) / b;
-      if ((st1 + p1 - 1) / p1 != a || (st2 + p2 - 1) / p2 != b) continue;  // no empty split
-      // rounds of one workgroup per CU, each as long as the longer split (~1.6 us per 32 k), plus the
-      // partial tiles written and read back at ~4 TB/s
-      const int64_t rounds = ((int64_t)a * pl.t1 + (int64_t)b * pl.t2 + 255) / 256;
-      const double cost = (double)rounds * (double)(p1 > p2 ? p1 : p2) * 1.6 +
-                          ((double)a * C * E + (double)b * C2 * C) * 8.0 / 4.0e6;
-      if (cost < best) {
-        best = cost;
-        pl.s1 = a;
-        pl.s2 = b;
-      }
+  // Split counts: the makespan of the launch's workgroups dispatched in order (the a t1 units of the
+  // first product, p1 stages each, then the b t2 of the second) onto 256 CUs one at a time (~2.8 us per
+  // 32-k stage), plus the partial tiles written and read back at ~4 TB/s.  Round 4's estimate (rounds x
+  // the longer split) missed that the second product's units start as soon as the first's free their CU:
+  // round 5 (tools/ab_enc_splits.py) configs[2] (3, 3) 136.9 vs its (2, 1) 141.7 us, configs[1] (8, 7)
+  // 30.0 vs (5, 4) 33.8, configs[3] (4, 1) 101.4 vs (8, 1) 106.2; the headline and configs[4] unchanged.
+  // Memoised per shape (the simulation is ~10^5 heap steps).
+  static std::mutex mu;
+  static std::map<std::pair<int64_t, int64_t>, std::pair<int, int>> memo;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = memo.find({E, C});
+    if (it != memo.end()) {
+      pl.s1 = it->second.first;
+      pl.s2 = it->second.second;
+    } else {
+      double best = 1e300;
+      pl.s1 = pl.s2 = 1;
+      std::vector<int64_t> slot(256);
+      for (int a = 1; a <= 32; ++a)
+        for (int b = 1; b <= 32; ++b) {
+          const int64_t p1 = (st1 + a - 1) / a, p2 = (st2 + b - 1) / b;
+          if ((st1 + p1 - 1) / p1 != a || (st2 + p2 - 1) / p2 != b) continue;  // no empty split
+          const int64_t n1 = (int64_t)a * pl.t1, n2 = (int64_t)b * pl.t2;
+          const int64_t q = n1 / 256, r = n1 % 256;
+          for (int i = 0; i < 256; ++i) slot[i] = (q + (i < r ? 1 : 0)) * p1;  // the first product round robin
+          std::make_heap(slot.begin(), slot.end(), std::greater<int64_t>());
+          int64_t span = (q + (r ? 1 : 0)) * p1;
+          for (int64_t i = 0; i < n2; ++i) {  // the second product onto the earliest free CU
+            std::pop_heap(slot.begin(), slot.end(), std::greater<int64_t>());
+            slot.back() += p2;
+            span = slot.back() > span ? slot.back() : span;
+            std::push_heap(slot.begin(), slot.end(), std::greater<int64_t>());
+          }
+          const double cost = (double)span * 2.8 + ((double)a * C * E + (double)b * C2 * C) * 8.0 / 4.0e6;
+          if (cost < best) {
+            best = cost;
+            pl.s1 = a;
+            pl.s2 = b;
+          }
+        }
+      memo[{E, C}] = {pl.s1, pl.s2};
     }
+  }
+  // lab knobs enc_s1 / enc_s2 (0: the planner's): force a split count (the chunks cover K, none empty)
+  if (mrp_host::tuning().enc_s1 > 0) pl.s1 = (int)(mrp_host::tuning().enc_s1 < st1 ? mrp_host::tuning().enc_s1 : st1);
+  if (mrp_host::tuning().enc_s2 > 0) pl.s2 = (int)(mrp_host::tuning().enc_s2 < st2 ? mrp_host::tuning().enc_s2 : st2);
   pl.kc1 = ((st1 + pl.s1 - 1) / pl.s1) * BK;
   pl.kc2 = ((st2 + pl.s2 - 1) / pl.s2) * BK;
+  pl.s1 = (int)((st1 * BK + pl.kc1 - 1) / pl.kc1);  // the splits the chunks give (no empty one)
+  pl.s2 = (int)((st2 * BK + pl.kc2 - 1) / pl.kc2);
   auto al = [](int64_t v) { return (v + 63) / 64 * 64; };  // 256-byte segments
   int64_t o = 0;
   pl.off_dzT = o;

@@ -110,6 +110,8 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"gemm_group", &t.gemm_group, 0, 64},
       {"nt_group", &t.nt_group, 0, 64},
       {"enc_bwd_psa", &t.enc_bwd_psa, 0, 2},
+      {"enc_s1", &t.enc_s1, 0, 64},
+      {"enc_s2", &t.enc_s2, 0, 64},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {

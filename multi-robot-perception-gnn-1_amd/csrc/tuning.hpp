@@ -52,6 +52,7 @@ struct Tuning {
   // mrp_edge_encoder_bwd_fused, given W2^T's packed image: 2 = both products read their A operand
   // pre-split (W2^T's image; dz^T written as an image by dzT_pack), 1 = only W2^T's, 0 = neither
   int enc_bwd_psa = 2;
+  int enc_s1 = 0, enc_s2 = 0;  // mrp_edge_encoder_bwd_fused: split counts of its two products (0: planner)
 };
 Tuning& tuning();
 

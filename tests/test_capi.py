@@ -188,7 +188,7 @@ def test_tuning_knobs_documented_in_the_header():
     try:
         for name, lo, hi in (("bwd_regular_mfma", 0, 1), ("bwd_complete_mfma", 0, 1), ("bwd_mfma_cpw", 1, 2),
                              ("bwd_pre2", 0, 2), ("fwd_regular_split", 0, 1), ("bwd_fused_cap", 1, 64),
-                             ("gemm_group", 0, 64), ("nt_group", 0, 64), ("enc_bwd_psa", 0, 2)):
+                             ("gemm_group", 0, 64), ("nt_group", 0, 64), ("enc_bwd_psa", 0, 2), ("enc_s1", 0, 64), ("enc_s2", 0, 64)):
             assert name.encode() in open(os.path.join(ROOT, "include", "mrp_gnn.h"), "rb").read() or \
                 name.startswith("bwd_fused")
             assert lib.mrp_tuning_set(name.encode(), lo) == 0
