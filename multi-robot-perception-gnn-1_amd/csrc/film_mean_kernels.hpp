@@ -1088,12 +1088,16 @@ __global__ void __launch_bounds__(kBlock, MINW) film_bwd_fused(AggArgs a) {
       const int vv = v < n ? v : n - 1;
       G[i] = load_frag<VEC, kOnePass>(at_bytes(gbase + (int64_t)vv * a.gs, lane_off));
     }
-    if (a.want_dgb) {
+    // x's rows, unconditionally: without a gamma/beta gradient (x may be null) they re-read grad_out's
+    // rows, unused.  Under `if (a.want_dgb)` the branch's join made hipcc copy the landed registers into
+    // place at its end — an s_waitcnt vmcnt(0) between this slice's loads and the next's, so PRE2's second
+    // slice set was only requested after the first had arrived (two dependent memory round trips)
+    const float* xb = a.want_dgb ? xbase : gbase;
+    const int64_t xstride = a.want_dgb ? a.xs : a.gs;
 #pragma unroll
-      for (int u = 0; u < NT; ++u) {
-        const int uu = u < n ? u : n - 1;
-        X[u] = load_frag<VEC, kOnePass>(at_bytes(xbase + (int64_t)uu * a.xs, lane_off));
-      }
+    for (int u = 0; u < NT; ++u) {
+      const int uu = u < n ? u : n - 1;
+      X[u] = load_frag<VEC, kOnePass>(at_bytes(xb + (int64_t)uu * xstride, lane_off));
     }
   };
   auto load_slice = [&](int vb, int j) { load_into(gv, xv, vb, j); };
