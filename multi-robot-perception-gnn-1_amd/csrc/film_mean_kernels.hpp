@@ -1653,8 +1653,12 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
       } else {
         const bool on = ok && jj < K;
         const int k = (node0 + (on ? pv : 0)) * K + (on ? jj : 0);
-        us[jj] = on ? a.src[k] - node0 : -1;
-        es[jj] = on ? a.eid[k] : -1;
+        // loaded unconditionally (k is a valid slot either way) and selected after: a load under the
+        // select became a branch whose join waited for it — one memory round trip per slot in turn
+        const int sv = a.src[k];
+        const int ev = a.eid[k];
+        us[jj] = on ? sv - node0 : -1;
+        es[jj] = on ? ev : -1;
       }
     }
   }
@@ -1722,17 +1726,20 @@ __global__ void __launch_bounds__(kBlock) film_bwd_mfma(AggArgs a) {
   if (nsteps > 0) load_step(0, gq, xn, bq);  // the first pixel group, ahead of the gamma loads
   if (pitem) {
     float gm[NE];
+    // every slot's gamma requested before any is used (edge 0 for an empty slot, discarded): under
+    // `es >= 0` each load was a branch whose join waited for it, NE round trips in turn
+    // (copy mode: gb may be null, so grad_out's first element is read and discarded instead)
+    float graw[NE];
+    const bool copy = a.mode == MRP_AGG_COPY_MEAN || a.gb == nullptr;
+    const float* gsrc = copy ? a.g : a.gb;
+#pragma unroll
+    for (int jj = 0; jj < NE; ++jj)
+      graw[jj] = gsrc[copy ? 0 : ((es[jj] >= 0 ? es[jj] : 0) * a.C + c0 + pcl) * 2];
 #pragma unroll
     for (int jj = 0; jj < NE; ++jj) {
-      gm[jj] = 0.f;
-      if (es[jj] >= 0) {
-        if (a.mode == MRP_AGG_COPY_MEAN) {
-          gm[jj] = 1.f;
-        } else {
-          gm[jj] = a.gb[(es[jj] * a.C + c0 + pcl) * 2];
-          if (a.logits) gm[jj] = sigmoidf(gm[jj]);
-        }
-      }
+      float gv = copy ? 1.f : graw[jj];
+      if (!copy && a.logits) gv = sigmoidf(gv);
+      gm[jj] = __int_as_float(__float_as_int(gv) & -(int)(es[jj] >= 0));  // es < 0 ? +0 : gv, by mask
     }
 #pragma unroll
     for (int u = 0; u < NPB; ++u) {

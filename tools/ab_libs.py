@@ -2,7 +2,7 @@
 """Kernel lab (not product code): the aggregation kernels of the product library (A) against a variant
 library (B, tools/build_variant_lib.py) in one process, alternated, HIP-graph timed like bench.py's
 rooflines (rotating buffer sets over 512 MB), at the headline and configs[1..4] shapes: forward,
-backward without a base and the training (DXB) backward.
+backward without a base and the training (DXB) backward; the backward's outputs compared bit for bit.
 usage: python tools/ab_libs.py tools/bin/<variant>.so [iters] [rounds]"""
 import ctypes
 import os
@@ -39,7 +39,9 @@ for name, B, N, C, H, knn in SHAPES:
 
     def run(lib, kind):
         _lib._lib = lib
-        if kind == "bwd":
+        if kind == "fwd":
+            fs = [lambda xi=xi, oi=G: mrp.film_mean_forward_into(xi, z, csr, mode, oi) for G, xi, _ in sets]
+        elif kind == "bwd":
             fs = [lambda G=G, xi=xi: mrp.aggregate.film_mean_backward(G, xi, z, csr, mode, True, True) for G, xi, _ in sets]
         else:
             fs = [lambda G=G, xi=xi, bs=bs: mrp.aggregate.film_mean_backward(G, xi, z, csr, mode, True, True,
@@ -48,7 +50,7 @@ for name, B, N, C, H, knn in SHAPES:
 
     for _ in range(rounds):
         for lab, lib in (("A", lib_a), ("B", lib_b)):
-            for kind in ("bwd", "dxb"):
+            for kind in ("fwd", "bwd", "dxb"):
                 res.setdefault((lab, kind), []).append(run(lib, kind))
     outs = {}
     for lab, lib in (("A", lib_a), ("B", lib_b)):
