@@ -247,6 +247,10 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
     for (int p = 0; p < 3; ++p) dst[p] = img[(int64_t)(min(hb, HB - 1) * 3 + p) * 64 + lane];
   };
   auto load_w1 = [&](int hb) { load_w1_into(hb, w1f); };
+  // all-X form, training: relu(X) of the wave's two hidden blocks kept here and h^T stored after the z
+  // loop, so the stores and their addressing do not sit between the W2 requests and the first z block
+  // (round 5, tools/ab_encoder_libs.py --train: 18.0 vs 18.5 us at the headline shape, bit-identical)
+  f16v Xk[2];
   auto x_store_from = [&](int buf, int hbx, const u4 (&wsrc)[3]) {
     bf8 wa[3];
 #pragma unroll
@@ -259,7 +263,9 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
     // every X of its edge block, so the column groups take the hidden blocks round robin and share the
     // stores (register i of lane (r, hh) is unit (i & 3) + 8 (i >> 2) + 4 hh of the block, edge e0 + r:
     // each register's 32 lanes store 128 contiguous bytes of a row)
-    if (a.hT != nullptr && hbx % ngroups == cg && hbx < HB && e0 + r < a.E) {
+    if constexpr (ALLX) {
+      Xk[buf] = X;
+    } else if (a.hT != nullptr && hbx % ngroups == cg && hbx < HB && e0 + r < a.E) {
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         a.hT[(int64_t)(hbx * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh) * a.hts + e0 + r] = relu(X[i]);
@@ -338,6 +344,17 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
       if (hb + 2 < HB) z_block((hb + 2) / NWV, (hb + 2) % NWV, f2);
       if (hb + 6 < HB) load_w2(hb + 6, f2);
       if (hb + 3 < HB) z_block((hb + 3) / NWV, (hb + 3) % NWV, f3);
+    }
+    if (a.hT != nullptr && e0 + r < a.E) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int hbx = w + q * NWV;
+        if (hbx < HB && hbx % ngroups == cg) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            a.hT[(int64_t)(hbx * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh) * a.hts + e0 + r] = relu(Xk[q][i]);
+        }
+      }
     }
   } else {
   __syncthreads();

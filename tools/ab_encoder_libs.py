@@ -1,7 +1,8 @@
 """Kernel lab (not product code): the one-launch encoder forward of the product library (A) against
 variant libraries (tools/build_variant_lib.py) at the headline and configs[1..4] encoder shapes,
-HIP-graph timed, libraries interleaved over rounds, logits compared for bit-identity.
-usage: python tools/ab_encoder_libs.py tools/bin/<variant>.so [...]"""
+HIP-graph timed, libraries interleaved over rounds, logits compared for bit-identity; with --train the
+training form (mrp_edge_encoder_fwd_split_train: logits and h^T, both compared).
+usage: python tools/ab_encoder_libs.py [--train] tools/bin/<variant>.so [...]"""
 import ctypes
 import os
 import sys
@@ -12,10 +13,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 import mrp_gnn_amd as mrp  # noqa: E402
 from mrp_gnn_amd import _lib  # noqa: E402
+from mrp_gnn_amd.aggregate import _ptr  # noqa: E402
 
 dev = torch.device("cuda:0")
+args = sys.argv[1:]
+train = "--train" in args
+args = [a for a in args if a != "--train"]
 libs = [("A", _lib.load_library())]
-for p in sys.argv[1:]:
+for p in args:
     lb = ctypes.CDLL(os.path.abspath(p))
     _lib._declare(lb)
     libs.append((os.path.basename(p), lb))
@@ -26,16 +31,28 @@ for name, E, C in [("head", 1792, 512), ("cfg1", 896, 512), ("cfg2", 1792, 1280)
     pose = (torch.randn(E, 9) * 8).to(dev)
     l1, l2 = enc.layers[0], enc.layers[2]
 
+    img = mrp.encoder.packed_weights(l1, l2)
+    z = torch.empty(E, 2 * C, device=dev)
+    hT = torch.empty(C, E, device=dev)
+    b2 = l2.bias.detach().contiguous()
+
     def f():
-        with torch.no_grad():
-            return mrp.encoder.encoder_forward_split(pose, l1, l2)
+        if not train:
+            with torch.no_grad():
+                return mrp.encoder.encoder_forward_split(pose, l1, l2)
+        lb = _lib._lib
+        _lib.check(lb.mrp_edge_encoder_fwd_split_train(
+            _ptr(pose), _ptr(img), _ptr(b2), E, C, _ptr(z), _ptr(hT), E,
+            ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "fwd_split_train")
+        return z, hT
     res, outs = {}, {}
     for _ in range(5):
         for lab, lb in libs:
             _lib._lib = lb
             res.setdefault(lab, []).append(bench.time_launches([f], 20, dev))
             if lab not in outs:
-                outs[lab] = f().clone()
+                o = f()
+                outs[lab] = torch.cat([t.reshape(-1).clone() for t in (o if isinstance(o, tuple) else (o,))])
     _lib._lib = libs[0][1]
     line = [f"{name} E={E} C={C}"]
     for lab, _ in libs:
