@@ -151,3 +151,34 @@ def test_fused_backward_w2t_image_bit_identical(cuda_device, E, C):
             assert torch.equal(grads[0][i], g[i]), i
         assert float((grads[0][3] - g[3]).abs().max()) <= 1e-6 * float(g[3].abs().max()) + 1e-7
     assert torch.equal(grads[1][3], grads[2][3])
+
+
+@pytest.mark.parametrize("E,C", [(1792, 512), (896, 512), (448, 2048), (224, 160)])
+def test_train_forward_writes_hidden(cuda_device, E, C):
+    """``mrp_edge_encoder_fwd_split_train`` directly: h^T (C, E) against relu(pose W1^T + b1) evaluated in
+    float64 with the fp32 yardstick, and the logits bit-identical to the inference kernel's — at the
+    headline shape (8 waves, every hidden block before z, h^T stored after the z loop) and at shapes
+    that take the round-by-round form (4 waves, or more hidden blocks than the LDS slots hold)."""
+    import ctypes
+
+    from mrp_gnn_amd.aggregate import _ptr
+    torch.manual_seed(E + C)
+    enc = m.edge_encoder([C, C]).to(cuda_device)
+    l1, l2 = enc.layers[0], enc.layers[2]
+    pose = (torch.randn(E, 9) * 8).to(cuda_device)
+    img = m.encoder.packed_weights(l1, l2)
+    z = torch.empty(E, 2 * C, device=cuda_device)
+    hT = torch.full((C, E), float("nan"), device=cuda_device)
+    lib = m.load_library()
+    m._lib.check(lib.mrp_edge_encoder_fwd_split_train(
+        _ptr(pose), _ptr(img), _ptr(l2.bias.detach().contiguous()), E, C, _ptr(z), _ptr(hT), E,
+        ctypes.c_void_p(torch.cuda.current_stream(cuda_device).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
+    with torch.no_grad():
+        z_inf = m.encoder.encoder_forward_split(pose, l1, l2)
+        h32 = torch.relu(torch.nn.functional.linear(pose, l1.weight, l1.bias)).t()
+        h64 = torch.relu(torch.nn.functional.linear(pose.double(), l1.weight.double(), l1.bias.double())).t()
+    torch.cuda.synchronize()
+    assert torch.equal(z, z_inf)
+    assert not torch.isnan(hT).any()
+    ok, errs = stack_ref.within(hT, h32, h64)
+    assert ok, errs
