@@ -72,7 +72,7 @@ Tuning& tuning() {
 
 extern "C" {
 
-int mrp_abi_version(void) { return 19; }
+int mrp_abi_version(void) { return 20; }
 
 int mrp_tuning_set(const char* name, int32_t value) {
   if (name == nullptr) return hipErrorInvalidValue;
@@ -112,6 +112,8 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"enc_bwd_psa", &t.enc_bwd_psa, 0, 2},
       {"enc_s1", &t.enc_s1, 0, 64},
       {"enc_s2", &t.enc_s2, 0, 64},
+      {"fused_producers", &t.fused_producers, 0, 4096},
+      {"fused_lab", &t.fused_lab, 0, 63},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {

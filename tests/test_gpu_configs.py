@@ -93,6 +93,62 @@ def test_config1_full_size(cuda_device):
     check_config(cuda_device, B=16, N=8, C=512, H=32, layers=2)
 
 
+def test_config0_own_shape_vs_oracle(cuda_device):
+    """configs[0]: the reference's CPU-runnable case (``dgl/training.py:28,176-218``) at its own shape —
+    B = 8 complete 4-robot graphs, C = 64, 32 x 32, one GCN layer (``dgl/model/models.py:207-226``) —
+    through the drop-in ``GCN`` on the HIP path, against the CPU oracle (``oracle.gcn_forward`` and
+    torch autograd through it) at the north-star 1e-5:
+      * the aggregation fed the oracle's own gamma/beta: bit-identical (each destination's sum over its 3
+        sources is sequential in source order, as in the reference's mailbox mean);
+      * the no-grad forward (the split-bf16 encoder, as bench.py's configs[0] record times it) and the
+        training forward;
+      * dx and the four edge-encoder parameter gradients (also held to float64 with the fp32 yardstick)."""
+    B, N, C, H = 8, 4, 64, 32
+    g = frames(B, N, C, H, H, seed=77)
+    torch.manual_seed(0)
+    gcn = m.GCN(types.SimpleNamespace(feature_dim=C))
+    params = {k: v.detach().clone() for k, v in gcn.edge_encoder.named_parameters()}
+    src, dst = (t.numpy() for t in g.edges())
+    x, pose = g.ndata["image"], g.edata["pose"]
+    # CPU oracle: forward and autograd through the reference op sequence
+    p_ref = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    x_ref = x.clone().requires_grad_(True)
+    ref = oracle.gcn_forward(p_ref, x_ref, pose, src, dst)
+    torch.manual_seed(1)
+    G = torch.randn_like(ref)
+    ref.backward(G)
+    gb_ref = oracle.edge_encoder_forward(params, pose)
+
+    gd = g.to(cuda_device)
+    gcn = gcn.to(cuda_device)
+    xd = gd.ndata["image"]
+    # the aggregation alone on the oracle's gamma/beta: the reference's rounding sequence
+    agg = m.film_mean(xd, gb_ref.to(cuda_device), gd.csr(cuda_device)).cpu()
+    assert torch.equal(agg, oracle.film_aggregate(x, gb_ref, src, dst))
+    with torch.no_grad():
+        out_eval = gcn(gd, xd).cpu()
+    assert rel_err(out_eval.numpy(), ref.detach().numpy()) <= 1e-5
+    xr = xd.detach().clone().requires_grad_(True)
+    out = gcn(gd, xr)
+    out.backward(G.to(cuda_device))
+    assert rel_err(out.detach().cpu().numpy(), ref.detach().numpy()) <= 1e-5
+    assert rel_err(xr.grad.cpu().numpy(), x_ref.grad.numpy()) <= 1e-5
+    # float64 yardstick for the parameter gradients (GEMM sums: any order is as good as fp32's)
+    sd, dd = (t.to(cuda_device).long() for t in g.edges())
+
+    def layer_grads(dtype):
+        p = {k: v.to(cuda_device, dtype).requires_grad_(True) for k, v in params.items()}
+        a = stack_ref.aggregate(xd.to(dtype), stack_ref.edge_gb(p, "", gd.edata["pose"]), sd, dd)
+        a.backward(G.to(cuda_device, dtype))
+        return {k: v.grad for k, v in p.items()}
+
+    g64, g32 = layer_grads(torch.float64), layer_grads(torch.float32)
+    for k, p in gcn.edge_encoder.named_parameters():
+        assert rel_err(p.grad.cpu().numpy(), p_ref[k].grad.numpy()) <= 1e-5, k
+        ok, e = stack_ref.within(p.grad, g32[k], g64[k])
+        assert ok, (k, e)
+
+
 def test_config1_shape_reduced_batch(cuda_device):
     """configs[1] (B=16, C=512, 32x32, 2 layers) at B=4: the 32x32 geometry (plane split forward,
     two-wave backward) through the whole stack."""

@@ -29,7 +29,9 @@ objs = []
 procs = []
 for s in b.SOURCES:
     o = os.path.join(tmp, os.path.basename(s) + ".o")
-    cmd = [b.hipcc(), f"--offload-arch={b.ARCH}"] + b.FLAGS + b.EXTRA_FLAGS.get(os.path.basename(s), []) + [
+    # LAB_FLAGS_<file stem>="-f... -f...": extra flags for one source of the variant
+    lab = os.environ.get("LAB_FLAGS_" + os.path.basename(s).split(".")[0], "").split()
+    cmd = [b.hipcc(), f"--offload-arch={b.ARCH}"] + b.FLAGS + b.EXTRA_FLAGS.get(os.path.basename(s), []) + lab + [
         "-I", os.path.join(ROOT, "include"), "-c", os.path.join(src, os.path.basename(s)), "-o", o]
     procs.append(subprocess.Popen(cmd))
     objs.append(o)
