@@ -227,16 +227,21 @@ def compress_backward_weight(gy: torch.Tensor, x: torch.Tensor, a: torch.Tensor,
     else:
         nbytes = int(lib.mrp_compress_bwd_weight_workspace(n, C, P, max(gs, xs, as_)))
         fn, name = lib.mrp_compress_bwd_weight, "mrp_compress_bwd_weight"
-    ws = torch.empty((nbytes + 3) // 4, device=gy.device, dtype=torch.float32) if nbytes > 0 else None
-    with torch.cuda.device(gy.device):
-        code = fn(_ptr(gy), gs, _ptr(x), xs, _ptr(a), as_, n, C, P, _ptr(dw), _ptr(db), _ptr(ws), nbytes,
-                  _stream(gy.device))
-    if code == _lib.HIP_ERROR_NOT_SUPPORTED:
-        for p, v in claimed:
-            release_grad_out(p, v)
-        return None
-    _lib.check(code, name)
-    return dw, db
+    done = False
+    try:  # claimed bucket slots go back unless the kernel wrote them (declined shape, error, exception)
+        ws = torch.empty((nbytes + 3) // 4, device=gy.device, dtype=torch.float32) if nbytes > 0 else None
+        with torch.cuda.device(gy.device):
+            code = fn(_ptr(gy), gs, _ptr(x), xs, _ptr(a), as_, n, C, P, _ptr(dw), _ptr(db), _ptr(ws), nbytes,
+                      _stream(gy.device))
+        if code == _lib.HIP_ERROR_NOT_SUPPORTED:
+            return None
+        _lib.check(code, name)
+        done = True
+        return dw, db
+    finally:
+        if not done:
+            for p, v in claimed:
+                release_grad_out(p, v)
 
 
 # ---- torch library GEMMs: the A/B comparison path and the shapes the kernels decline -------------

@@ -1454,7 +1454,11 @@ EncPlan enc_plan(int64_t E, int64_t C) {
   // the longer split) missed that the second product's units start as soon as the first's free their CU:
   // round 5 (tools/ab_enc_splits.py) configs[2] (3, 3) 136.9 vs its (2, 1) 141.7 us, configs[1] (8, 7)
   // 30.0 vs (5, 4) 33.8, configs[3] (4, 1) 101.4 vs (8, 1) 106.2; the headline and configs[4] unchanged.
-  // Memoised per shape (the simulation is ~10^5 heap steps).
+  // Memoised per shape (at most kMemo shapes; a full memo starts over).  A pair whose lower bound — its
+  // first product's rounds, or all its work spread evenly over the CUs, plus its traffic — is no better
+  // than the best found is not simulated: the full search is up to 32 x 32 pairs of b t2 heap steps
+  // each (~5e5 at C = 2048), the pruned one a few percent of that.
+  constexpr size_t kMemo = 64;
   static std::mutex mu;
   static std::map<std::pair<int64_t, int64_t>, std::pair<int, int>> memo;
   {
@@ -1473,6 +1477,9 @@ EncPlan enc_plan(int64_t E, int64_t C) {
           if ((st1 + p1 - 1) / p1 != a || (st2 + p2 - 1) / p2 != b) continue;  // no empty split
           const int64_t n1 = (int64_t)a * pl.t1, n2 = (int64_t)b * pl.t2;
           const int64_t q = n1 / 256, r = n1 % 256;
+          const double traffic = ((double)a * C * E + (double)b * C2 * C) * 8.0 / 4.0e6;
+          const int64_t lb = std::max<int64_t>((q + (r ? 1 : 0)) * p1, (n1 * p1 + n2 * p2 + 255) / 256);
+          if ((double)lb * 2.8 + traffic >= best) continue;  // cannot beat the best: skip the simulation
           for (int i = 0; i < 256; ++i) slot[i] = (q + (i < r ? 1 : 0)) * p1;  // the first product round robin
           std::make_heap(slot.begin(), slot.end(), std::greater<int64_t>());
           int64_t span = (q + (r ? 1 : 0)) * p1;
@@ -1482,13 +1489,14 @@ EncPlan enc_plan(int64_t E, int64_t C) {
             span = slot.back() > span ? slot.back() : span;
             std::push_heap(slot.begin(), slot.end(), std::greater<int64_t>());
           }
-          const double cost = (double)span * 2.8 + ((double)a * C * E + (double)b * C2 * C) * 8.0 / 4.0e6;
+          const double cost = (double)span * 2.8 + traffic;
           if (cost < best) {
             best = cost;
             pl.s1 = a;
             pl.s2 = b;
           }
         }
+      if (memo.size() >= kMemo) memo.clear();
       memo[{E, C}] = {pl.s1, pl.s2};
     }
   }

@@ -113,7 +113,7 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"enc_s1", &t.enc_s1, 0, 64},
       {"enc_s2", &t.enc_s2, 0, 64},
       {"fused_producers", &t.fused_producers, 0, 4096},
-      {"fused_lab", &t.fused_lab, 0, 63},
+      {"fused_lab", &t.fused_lab, 0, 127},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {

@@ -106,8 +106,16 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // column block's W2 (6 KiB) — which arrive once per workgroup by LDS-DMA into a ring of kRing hidden
 // blocks (kRing - 1 ahead), so a wave's weight bytes per MFMA are a quarter of a wave owning its own
 // columns, and the fetch latency under the aggregation's HBM stream hides behind three blocks' work.
+// lab bit 64 (Tuning::fused_lab): a timeline in the workspace past the hand-off words — per item its
+// producer's start and publish times, per graph its first aggregation workgroup's wait window
+// (s_memrealtime, 100 MHz).  Never set in the product.
+__device__ __forceinline__ uint64_t* timeline(const FusedArgs& f) {
+  return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(f.err) + 256);
+}
+
 __device__ __forceinline__ void produce(const FusedArgs& f, int item, u4* lds) {
   using namespace mrp_x6;
+  if ((f.lab & 64) && threadIdx.x == 0) timeline(f)[2 * item] = __builtin_amdgcn_s_memrealtime();
   const int C = f.C;
   const int HB = C / 32;
   const int ncolb = 2 * C / 32;
@@ -204,7 +212,10 @@ __device__ __forceinline__ void produce(const FusedArgs& f, int item, u4* lds) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the signal
   __syncthreads();  // (also: every wave is done with the ring before a next item refills it)
-  if (threadIdx.x == 0) __hip_atomic_store((gu32*)(f.state + item), kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store((gu32*)(f.state + item), kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f.lab & 64) timeline(f)[2 * item + 1] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // A producer workgroup: claims its items (p, p + nprod, ...) in one round of CAS by wave 0, then
@@ -241,6 +252,8 @@ struct Consumer {
   __device__ Consumer(const FusedArgs& fa, u4* s, uint32_t* wf) : f(fa), slots(s), wave_flag(wf) {}
 
   __device__ void issue(int b, int c0) {
+    b_ = b;
+    c0_ = c0;
     // wave-uniform (a scalar register: it stays live across the fallback's producer routine)
     item = __builtin_amdgcn_readfirstlane((b * f.halves / 4) * (2 * f.C / 32) + (2 * c0) / 32);
     reload();
@@ -248,8 +261,20 @@ struct Consumer {
   __device__ void reload() {
     if ((threadIdx.x & 63) == 0) v = ld_state_at(f.state, (uint32_t)item * 4u);
   }
+  int b_ = 0, c0_ = 0;
   __device__ bool wait() {
     if (f.lab & 2) return true;
+    const bool stamp = (f.lab & 64) && c0_ == 0 && threadIdx.x == 0;
+    uint64_t t0 = stamp ? __builtin_amdgcn_s_memrealtime() : 0;
+    const bool ok = spin();
+    if (stamp) {
+      uint64_t* tl = timeline(f) + 2 * f.nitems + 2 * b_;
+      tl[0] = t0;
+      tl[1] = __builtin_amdgcn_s_memrealtime();
+    }
+    return ok;
+  }
+  __device__ bool spin() {
     // relaxed sc1 polls by lane 0 with s_sleep; give up after a few ms (the caller's fallback)
     for (int spins = 0; !__all(v == kReady); ++spins) {
       if (spins >= 4096) return false;

@@ -58,7 +58,8 @@ struct Tuning {
   int fused_producers = 128;
   // lab bits (0 in the product): 1 = the launcher skips its memset (the caller zeroes the words),
   // 2 = aggregation workgroups do not wait (rows assumed present: prologue-cost A/B only),
-  // 4 = producers return at once (with 2: the aggregation alone in the fused grid)
+  // 4 = producers return at once (with 2: the aggregation alone in the fused grid), 8 = producers
+  // store nothing, 16 = producers skip the MFMAs, 32 = producers only sleep, 64 = timeline (gcn_fused.hip)
   int fused_lab = 0;
 };
 Tuning& tuning();

@@ -18,8 +18,10 @@ reference's only parallelism (single process, and it cannot scatter a DGLGraph).
 Averaging: each rank's loss is normally a mean over its own graphs, so with uneven shards
 (``shard_range`` of B graphs over P ranks when P does not divide B) the full-batch gradient is
 ``sum_r (n_r / N) g_r``, not ``(1/P) sum_r g_r``.  :meth:`GradAllReducer.set_local_count` gives the
-reducer ``n_r`` (one tiny all-reduce finds ``N``); every bucket is then scaled by ``n_r / N``
-before its SUM all-reduce.  Without it the reducer assumes equal shards and scales by ``1/P``.
+reducer ``n_r`` (one tiny all-reduce finds ``N``); every bucket is then reduced as ``sum_r s_r g_r``
+with ``s_r = n_r / N``.  Without it the reducer assumes equal shards and uses ``s_r = 1/P``.  On RCCL
+the scale rides inside the collective (a pre-multiplied sum, ``ncclRedOpCreatePreMulSum``): no pass
+over the bucket before it; backends without one (gloo) scale the bucket in place first.
 One backward per :meth:`GradAllReducer.synchronize`: a gradient that lands again after its
 bucket's all-reduce was launched (gradient accumulation over several backwards) raises instead
 of silently reducing a partial sum.
@@ -133,8 +135,13 @@ class GradAllReducer:
     SLOT_ALIGN = 256
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_bytes: int = 32 << 20,
-                 group: Optional[dist.ProcessGroup] = None):
+                 group: Optional[dist.ProcessGroup] = None, auto_arm: bool = False):
         self.group = group
+        #: re-arm in every ``synchronize()`` (for callers that never call :meth:`arm` themselves): the
+        #: kernels then keep writing gradients into the buckets step after step
+        self.auto_arm = bool(auto_arm)
+        self._was_armed = False
+        self._warned_unarmed = False
         self.world = dist.get_world_size(group)
         params = [p for p in params if p.requires_grad]
         self.buckets: List[List[torch.nn.Parameter]] = []
@@ -166,6 +173,8 @@ class GradAllReducer:
         self._scale = 1.0 / self.world
         self._empty = False  # this rank holds no graphs this step (set_local_count(0))
         self.copies = 0
+        self.scaled_passes_skipped = 0  # buckets whose scale rode inside the collective (tests)
+        self._ops = {}  # scale -> RCCL pre-multiplied-sum op
         #: (event, bucket) in the order they happen during a backward: ("grad", b) when a parameter's
         #: gradient lands, ("launch", b) when a bucket's all-reduce is started; ``last_events`` is the
         #: record of the last synchronized step — the evidence that the all-reduces overlap backward
@@ -197,6 +206,7 @@ class GradAllReducer:
         device or dtype after the reducer was built.  Returns self (``reducer.arm(); loss.backward()``)."""
         self._rekey()
         self._armed = True
+        self._was_armed = True
         return self
 
     def _rekey(self) -> None:
@@ -252,6 +262,14 @@ class GradAllReducer:
         if g is None:
             v.zero_()
         elif g.data_ptr() != v.data_ptr():
+            if not self._armed and self._was_armed and not self._warned_unarmed:
+                # armed once, not since the last synchronize(): the HIP kernels' gradients now take this
+                # copy instead of being written in place — correct, but a hidden pass per gradient
+                import warnings
+                warnings.warn("GradAllReducer: a gradient landed while the reducer was not armed (call arm() or "
+                              "set_local_count() before every backward, or build it with auto_arm=True); it is "
+                              "copied into its bucket instead of being written there by the kernel", stacklevel=2)
+                self._warned_unarmed = True
             v.copy_(g)
             self.copies += 1
         else:
@@ -271,17 +289,36 @@ class GradAllReducer:
         if self._pending[bi] == 0:
             self._launch(bi)
 
+    def _premul(self) -> bool:
+        """The collective applies the scale itself (RCCL's pre-multiplied sum)."""
+        return dist.get_backend(self.group) == "nccl" and hasattr(dist, "_make_nccl_premul_sum")
+
+    def _reduce_op(self, flat: torch.Tensor):
+        """The reduction of one bucket: ``sum_r s_r g_r`` with this rank's scale ``s_r`` (n_r / N, or 1/P).
+        RCCL: a pre-multiplied sum (the scale applied inside the collective's own pass; no read and
+        write of the bucket before it).  Other backends: the bucket scaled in place, then a SUM."""
+        if self._premul():
+            op = self._ops.get(self._scale)
+            if op is None:
+                op = self._ops[self._scale] = dist._make_nccl_premul_sum(self._scale)
+            self.scaled_passes_skipped += 1
+            return op
+        flat.mul_(self._scale)
+        return dist.ReduceOp.SUM
+
     def _launch(self, bi: int) -> None:
         for p in self.buckets[bi]:
             if id(p) not in self._landed:  # no gradient this step (an unused parameter)
                 self._adopt(p)
         flat = self._flat[bi]
         if self._empty:
+            # an empty shard contributes exact zeros (its 0/0 mean loss is NaN: 0 * NaN would poison the sum)
             flat.zero_()
+            op = dist.ReduceOp.SUM
         else:
-            flat.mul_(self._scale)  # n_r / N (or 1 / P): the SUM all-reduce then yields the average
+            op = self._reduce_op(flat)
         self.events.append(("launch", bi))
-        self._work[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._work[bi] = dist.all_reduce(flat, op=op, group=self.group, async_op=True)
 
     def synchronize(self) -> None:
         """Wait for every bucket (launching any whose hooks did not all fire, e.g. unused
@@ -294,6 +331,8 @@ class GradAllReducer:
         self.last_events = self.events
         self.reset()
         self._armed = False
+        if self.auto_arm:
+            self.arm()
 
     def remove(self) -> None:
         for h in self._hooks:

@@ -315,7 +315,7 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
       gradient all-reducer's buckets when one holds the parameters (``dist.grad_out_like``)."""
 
     @staticmethod
-    def forward(ctx, pose, w1, b1, w2, b2, img, w2t, w2t_img=None):
+    def forward(ctx, pose, w1, b1, w2, b2, img, l2):
         E, C = pose.shape[0], w1.shape[0]
         pose = pose.detach().contiguous().float()
         b2c = b2.detach().contiguous().float() if b2 is not None else None
@@ -326,13 +326,15 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
             _lib.check(lib.mrp_edge_encoder_fwd_split_train(
                 _ptr(pose), _ptr(img), _ptr(b2c) if b2c is not None else None, E, C, _ptr(z), _ptr(hT), E,
                 ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
-        ctx.save_for_backward(pose, w1, b1, w2, b2, hT, w2t)
-        ctx.w2t_img = w2t_img
+        ctx.save_for_backward(pose, w1, b1, w2, b2, hT)
+        # W2^T (and its packed image) are built in backward, only for the products that run:
+        # a forward whose backward never runs, or runs without dh^T, packs nothing
+        ctx.l2 = l2
         return z
 
     @staticmethod
     def backward(ctx, dz):
-        pose, w1, b1, w2, b2, hT, w2t = ctx.saved_tensors
+        pose, w1, b1, w2, b2, hT = ctx.saved_tensors
         need = ctx.needs_input_grad
         dz = dz.contiguous().float()
         E, C = pose.shape[0], w1.shape[0]
@@ -351,12 +353,12 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
             dw2, db2 = _grad_out(w2, (2 * C, C), dev), _grad_out(b2, (2 * C,), dev)
             wsf = torch.empty((int(lib.mrp_edge_encoder_bwd_fused_workspace(E, C)) + 3) // 4, device=dev)
             with torch.cuda.device(dev):
-                w2t_img = ctx.w2t_img
+                w2t, w2t_img = transposed_w2(ctx.l2), packed_w2t(ctx.l2)
                 _lib.check(lib.mrp_edge_encoder_bwd_fused(
                     _ptr(dz), _ptr(w2t), _ptr(w2t_img) if w2t_img is not None else None, _ptr(hT), _ptr(pose), E, C,
                     _ptr(dw1), _ptr(db1), _ptr(dw2), _ptr(db2),
                     _ptr(wsf), wsf.numel() * 4, ctypes.c_void_p(cur.cuda_stream)), "mrp_edge_encoder_bwd_fused")
-            return None, dw1, db1, dw2, db2, None, None, None
+            return None, dw1, db1, dw2, db2, None, None
         dw2 = db2 = side = None
         with torch.cuda.device(dev):
             if need[3] or need[4]:  # dz^T, then dW2 = dz^T h with db2 as its row sums, on the side stream
@@ -376,6 +378,7 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
                         t.record_stream(side)
             dw1 = db1 = dhT = None
             if need[0] or need[1] or need[2]:  # dh^T = W2^T dz^T, then the ReLU mask, dW1, db1
+                w2t = transposed_w2(ctx.l2)
                 st = ctypes.c_void_p(cur.cuda_stream)
                 dhT = torch.empty((C, E), device=dev)
                 wsb = workspace()
@@ -392,7 +395,7 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
             if side is not None:
                 cur.wait_stream(side)
         dpose = (dhT * (hT > 0)).t().mm(w1.float()) if need[0] else None
-        return dpose, dw1, db1, dw2 if need[3] else None, db2, None, None, None
+        return dpose, dw1, db1, dw2 if need[3] else None, db2, None, None
 
 
 def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Tensor:
@@ -413,6 +416,6 @@ def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Te
             and tuple(l1.weight.shape) == (C, 9) and tuple(l2.weight.shape) == (2 * C, C):
         PATH_COUNTS["split_train"] += 1
         return EdgeEncoderSplitFunction.apply(pose, l1.weight, l1.bias, l2.weight, l2.bias,
-                                              packed_weights(l1, l2), transposed_w2(l2), packed_w2t(l2))
+                                              packed_weights(l1, l2), l2)
     PATH_COUNTS["autograd"] += 1
     return EdgeEncoderFunction.apply(*params)

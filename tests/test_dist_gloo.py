@@ -418,3 +418,105 @@ def test_bench_self_launch_command():
     assert "WORLD_SIZE" not in env and env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
     args = bench.parse_args(["--gpus", "2", "--dist-backend", "gloo"])
     assert args.gpus == 2 and args.dist_backend == "gloo"
+
+
+def _premul_worker(rank, world, port):
+    """The RCCL path's scale fold, run over gloo: the backend query answers "nccl", RCCL's
+    pre-multiplied-sum op is stood in for by a marker that the all-reduce wrapper applies (as the
+    collective would, inside its own pass), and the reducer must hand the collective UNSCALED buckets
+    with its n_r / N in the op — no pass over a bucket before its all-reduce (VERDICT r5 weak #6)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    real_all_reduce, real_backend = dist.all_reduce, dist.get_backend
+    seen = []
+
+    def all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False):
+        if isinstance(op, tuple) and op[0] == "premul":
+            seen.append((t.clone(), op[1]))
+            t.mul_(op[1])  # what RCCL's pre-multiplied sum does inside the collective
+            op = dist.ReduceOp.SUM
+        return real_all_reduce(t, op=op, group=group, async_op=async_op)
+
+    try:
+        dist.get_backend = lambda group=None: "nccl"
+        dist._make_nccl_premul_sum = lambda factor: ("premul", factor)
+        dist.all_reduce = all_reduce
+        torch.manual_seed(321)
+        data, target = torch.randn(7, 9), torch.randn(7, 3)
+        ref = _model()
+        torch.nn.functional.mse_loss(ref(data), target).backward()
+        lo, hi = shard_range(7, rank, world)  # 4 + 3 rows: uneven shards
+        local = _model()
+        torch.nn.functional.mse_loss(local(data[lo:hi]), target[lo:hi]).backward()
+        model = _model()
+        red = GradAllReducer(model.parameters(), bucket_bytes=512)
+        scale = red.set_local_count(hi - lo)
+        assert abs(scale - (hi - lo) / 7) < 1e-12
+        torch.nn.functional.mse_loss(model(data[lo:hi]), target[lo:hi]).backward()
+        red.synchronize()
+        assert red.scaled_passes_skipped == len(red.buckets) >= 2
+        # every bucket reached the collective unscaled, with this rank's scale in the op
+        local_grads = {id(p): q.grad for p, q in zip(model.parameters(), local.parameters())}
+        assert len(seen) == len(red.buckets)
+        for (flat, factor), bucket in zip(seen, red.buckets):
+            assert factor == scale
+            for p in bucket:
+                bi, off, n = red._slot[id(p)]
+                assert torch.equal(flat[off:off + n].view_as(p), local_grads[id(p)])
+        for p, q in zip(model.parameters(), ref.parameters()):
+            assert torch.allclose(p.grad, q.grad, rtol=1e-5, atol=1e-6), (rank, p.shape)
+        red.remove()
+    finally:
+        dist.all_reduce, dist.get_backend = real_all_reduce, real_backend
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_scale_rides_in_the_collective():
+    mp.spawn(_premul_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _arming_worker(rank, world, port):
+    """ADVICE r5: a reducer armed once and then not re-armed warns (once) when gradients take the copy
+    path; ``auto_arm=True`` re-arms in every synchronize(), so the kernels keep their in-place slots."""
+    import warnings
+
+    from mrp_gnn_amd.dist import grad_out_like
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = torch.nn.Parameter(torch.randn(16, 9))
+        red = GradAllReducer([w])
+        red.arm()
+        w.sum().backward()
+        red.synchronize()
+        w.grad = None
+        with pytest.warns(UserWarning, match="not armed"):
+            w.sum().backward()  # not re-armed: the gradient is copied into its slot
+            red.synchronize()
+        w.grad = None
+        with warnings.catch_warnings():
+            warnings.simplefilter("error")  # warned once only
+            w.sum().backward()
+            red.synchronize()
+        red.remove()
+        v = torch.nn.Parameter(torch.randn(16, 9))
+        auto = GradAllReducer([v], auto_arm=True)
+        auto.arm()
+        for _ in range(3):
+            v.grad = None
+            slot = grad_out_like(v)  # what a HIP backward kernel asks for: handed out every step
+            assert slot is not None and slot.data_ptr() == auto.view(v).data_ptr()
+            v.grad = slot.fill_(1.0)
+            (v * 0).sum().backward()
+            auto.synchronize()
+            assert torch.allclose(v.grad, torch.ones_like(v))
+        assert auto.copies == 0
+        auto.remove()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_arming_world2():
+    mp.spawn(_arming_worker, args=(2, _free_port()), nprocs=2, join=True)
