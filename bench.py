@@ -136,6 +136,39 @@ def time_launches(launches, iters, device):
     return times[2] / iters * 1e-3  # seconds
 
 
+def copy_ceiling(plane_bytes, device, iters):
+    """The same box's streaming ceiling at a kernel's plane bytes, timed exactly like the kernels
+    (HIP graph over rotating buffer sets > 512 MB, median of replays): ``mrp_stream_copy`` of
+    ``plane_bytes`` (one read and one write of each byte, nontemporal float4).  Returns its record;
+    ``ceiling_frac`` of a kernel = its achieved GB/s over this copy's (a driver
+    number that is low against 8 TB/s but level with this reads as the box, not as a regression)."""
+    lib = mrp.load_library()
+    n = plane_bytes // 4
+    sets = rotating_sets(2 * plane_bytes)
+    bufs = [(torch.empty(n, device=device), torch.empty(n, device=device)) for _ in range(sets)]
+    for a, _ in bufs:
+        a.normal_()
+    nb = n * 4 // 16 * 16
+
+    def launch(a, b):
+        code = lib.mrp_stream_copy(a.data_ptr(), b.data_ptr(), nb, torch.cuda.current_stream(device).cuda_stream)
+        if code != 0:
+            raise RuntimeError(f"mrp_stream_copy failed: {code}")
+
+    t = time_launches([lambda a=a, b=b: launch(a, b) for a, b in bufs], iters, device)
+    del bufs
+    ach = 2 * nb / t / 1e9
+    return {"kernel": "mrp_stream_copy (1 read + 1 write, float4, nontemporal)", "bytes": 2 * nb, "us": t * 1e6,
+            "achieved": ach, "frac": ach / HBM_PEAK_GBS, "rotating_sets": sets}
+
+
+def with_ceiling(rec, ceil):
+    """Attach the copy yardstick: the kernel's achieved GB/s as a fraction of the copy's on this box."""
+    rec["ceiling_frac"] = rec["achieved"] / ceil["achieved"]
+    rec["copy_ceiling_frac_of_peak"] = ceil["frac"]
+    return rec
+
+
 def roofline(kernel, bytes_launch, t, traffic=None, traffic_src=None, **extra):
     achieved = bytes_launch / t / 1e9
     r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -466,6 +499,9 @@ def config_record(cid, world, rank, device, args):
     rec["roofline_fwd"] = roofline(kname, alg_bytes_fwd(Nt, E, C, P), tf, rotating_sets=nf,
                                    footprint_mb=round(nf * (2 * plane) / 2**20))
     del sets, launches
+    ceil = copy_ceiling(plane, device, args.kernel_iters)
+    rec["copy_ceiling"] = ceil
+    with_ceiling(rec["roofline_fwd"], ceil)
     # the backward as training runs it (FilmCompressFunction: x's compress gradient is the base that
     # the kernel adds into dx, the DXB instantiation), and without the base for comparison
     nb = rotating_sets(4 * plane + 2 * E * 2 * C * 4)
@@ -478,13 +514,14 @@ def config_record(cid, world, rank, device, args):
     bname = (("film_bwd_mfma" if P % 64 == 0 else "film_bwd_regular") if knn and N > 8 else "film_bwd_fused")
     launches = [lambda G=G, xi=xi, bs=bs: bwd(G, xi, bs) for G, xi, bs in bsets]
     tb = time_launches(launches, args.kernel_iters, device)
-    rec["roofline_bwd"] = roofline(bname, alg_bytes_bwd(Nt, E, C, P, base=True), tb, rotating_sets=nb,
-                                   footprint_mb=round(nb * (4 * plane) / 2**20),
-                                   form="training: grad_x base added in-kernel (the DXB instantiation)")
+    rec["roofline_bwd"] = with_ceiling(roofline(bname, alg_bytes_bwd(Nt, E, C, P, base=True), tb, rotating_sets=nb,
+                                                footprint_mb=round(nb * (4 * plane) / 2**20),
+                                                form="training: grad_x base added in-kernel (the DXB instantiation)"),
+                                       ceil)
     launches = [lambda G=G, xi=xi: bwd(G, xi, None) for G, xi, _ in bsets]
     tb0 = time_launches(launches, args.kernel_iters, device)
-    rec["roofline_bwd_no_base"] = roofline(bname, alg_bytes_bwd(Nt, E, C, P), tb0, rotating_sets=nb,
-                                           footprint_mb=round(nb * (3 * plane) / 2**20))
+    rec["roofline_bwd_no_base"] = with_ceiling(roofline(bname, alg_bytes_bwd(Nt, E, C, P), tb0, rotating_sets=nb,
+                                                        footprint_mb=round(nb * (3 * plane) / 2**20)), ceil)
     del bsets, launches
     return rec
 
@@ -592,6 +629,8 @@ def main():
         mode = mrp._lib.MODE_FILM_MEAN | mrp._lib.GB_LOGITS
         t_kernel = time_launches([lambda: mrp.film_mean_forward_into(x, z, csr, mode, out)], args.kernel_iters,
                                  device)
+        del out
+        ceil_h = copy_ceiling(Nt * C * P * 4, device, args.kernel_iters)
 
     train = None if args.no_train else train_step_time(gcn, g, x, world, device, args)
     configs = {}
@@ -625,8 +664,10 @@ def main():
         "data": "synthetic (seeded complete 8-robot graphs, relative poses from random robot poses, randn features)",
         "config": {"workload": workload, "graphs_per_rank": B, "global_graphs": B * world, "robots": N,
                    "channels": C, "H": H, "W": W, "layers": 1, "parallelism": f"dp{world} (independent graphs)"},
-        "roofline": roofline("film_fwd", bytes_launch, t_kernel, traffic, traffic_src,
-                             read_frac=(bytes_launch - Nt * C * P * 4) / t_kernel / 1e9 / HBM_PEAK_GBS),
+        "roofline": with_ceiling(roofline("film_fwd", bytes_launch, t_kernel, traffic, traffic_src,
+                                          read_frac=(bytes_launch - Nt * C * P * 4) / t_kernel / 1e9 / HBM_PEAK_GBS),
+                                 ceil_h),
+        "copy_ceiling": ceil_h,
     }
     if train is not None:
         t_train, reducer_buckets = train

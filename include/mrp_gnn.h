@@ -408,27 +408,6 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
                           float* edge_pose, int32_t* indptr, int32_t* src, int32_t* eid,
                           int32_t* graph_off, void* stream);
 
-/* The no-grad GCN layer in ONE launch (gcn_fused.hip): replaces edge_encoder(pose) (models.py:222,
- * dgl/model/models.py:146-154) + update_all(edge_udf, node_udf) (models.py:223) of GCN.forward
- * (models.py:219-226) on complete graphs — what mrp_edge_encoder_fwd_split followed by
- * mrp_film_mean_fwd (MRP_AGG_FILM_MEAN | MRP_AGG_GB_LOGITS, MRP_GRAPH_COMPLETE) compute, bit for bit:
- * the first workgroups of the grid compute the encoder's logits graph by graph on the matrix cores
- * while the others aggregate, each waiting only for its own graph's rows (agent-scope hand-off).
- *   x, out     (num_graphs*max_nodes, C, P) fp32, 16-byte aligned, node strides multiples of 4
- *   pose       (E, 9) edge poses, E = num_graphs*max_nodes*(max_nodes-1) (MRP_GRAPH_COMPLETE order)
- *   packed     mrp_edge_encoder_pack's image of (W1, b1, W2); b2 (2C) or NULL
- *   z          (E, 2C) fp32: receives the logits (the reference's pre-Sigmoid encoder output)
- *   workspace  >= mrp_gcn_fwd_fused_workspace_bytes(num_graphs, max_nodes, C, P) bytes, 16-byte
- *              aligned; the call zeroes its hand-off words (a memset node) before the kernel
- * Shapes: 2 <= max_nodes <= 8, C % 32 == 0, P % 4 == 0 with 256-thread aggregation workgroups (planes of
- * >= 64 pixels), E*2C*4 < 2^31; any other shape returns
- * hipErrorNotSupported (the two-launch path serves it).  mrp_gcn_fwd_fused_workspace_bytes returns 0
- * for a shape the call declines.  Graph-capturable (a memset node and a kernel node). */
-int64_t mrp_gcn_fwd_fused_workspace_bytes(int32_t num_graphs, int32_t max_nodes, int32_t C, int32_t P);
-int mrp_gcn_fwd_fused(const float* x, int64_t x_node_stride, const float* pose, const void* packed, const float* b2,
-                      int32_t num_graphs, int32_t max_nodes, int32_t C, int32_t P, float* z, float* out,
-                      int64_t out_node_stride, void* workspace, int64_t workspace_bytes, void* stream);
-
 /* Experiment knobs of the launchers (kernel-lab sweeps; not needed for normal use; process-wide,
  * not thread-safe).  Returns hipErrorInvalidValue for an unknown name or a value out of range;
  * "reset" restores every default.  Geometry: "fwd_lo"/"fwd_hi"/"fwd_cap", "fwd_regular_*",
@@ -450,12 +429,13 @@ int mrp_gcn_fwd_fused(const float* x, int64_t x_node_stride, const float* pose, 
  * forward / data gradient, "nt_group" (the same, default 0) for the weight gradient; "enc_bwd_psa"
  * (mrp_edge_encoder_bwd_fused given w2T_packed: 2 default = both products read their A operand
  * pre-split, dz^T written as a packed image; 1 = only W2^T's image; 0 = both split in the kernel);
- * "enc_s1" / "enc_s2" (its two products' split-K counts, 0 = the planner's); "fused_producers"
- * (mrp_gcn_fwd_fused: encoder workgroups, default 128). */
+ * "enc_s1" / "enc_s2" (its two products' split-K counts, 0 = the planner's). */
 int mrp_tuning_set(const char* name, int32_t value);
 
-/* Library identification: ABI version (incremented on signature changes; 20 = this header: v19 plus
- * the one-launch no-grad GCN layer (mrp_gcn_fwd_fused + workspace); 19: v18 with
+/* Library identification: ABI version (incremented on signature changes; 21 = this header: v19 plus
+ * the streaming yardstick mrp_stream_copy; 20: v19 plus a one-launch no-grad GCN layer
+ * (mrp_gcn_fwd_fused), measured slower than the two launches it replaced and removed in 21
+ * (tools/lab_patches/r06_fused_layer.patch); 19: v18 with
  * mrp_edge_encoder_bwd_fused taking W2^T's packed image (w2T_packed); 18: v17 without
  * mrp_edge_encoder_fwd (the fp32 one-launch encoder, superseded by mrp_edge_encoder_fwd_split) and
  * with fewer tuning knobs (only those that select kernels the library builds); 17: v16 plus
@@ -471,6 +451,12 @@ int mrp_tuning_set(const char* name, int32_t value);
  * compress kernels, their weight packing and mrp_film_gate are gone), and the edge encoder's
  * second Linear and whole forward, mrp_edge_logits_fwd / mrp_edge_encoder_fwd). */
 int mrp_abi_version(void);
+
+/* The streaming yardstick the benchmark reports beside every aggregation roofline (ceiling_frac):
+ * dst = src over `bytes` (a multiple of 16; 16-byte aligned pointers) as one nontemporal 16-byte load
+ * and store per thread — the 1-read-1-write copy the HBM-bound kernels are measured against on the
+ * same box in the same run.  Not part of the GCN path. */
+int mrp_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);
 
 /* Human-readable text for a return code (static storage). */
 const char* mrp_error_string(int code);

@@ -9,7 +9,7 @@ name is not a Python identifier).
 from ._lib import MAX_NODES, MAX_REGULAR_K, MODES, graph_regular, load_library  # noqa: F401
 from .aggregate import (EpilogueSpec, FilmMeanFunction, film_mean, film_mean_cat,  # noqa: F401
                         film_mean_cat_forward_into, film_mean_forward_into, film_mean_mix, film_mean_residual)
-from . import compat, compress, encoder, fused  # noqa: F401
+from . import compat, compress, encoder  # noqa: F401
 from .device_graph import frame_batch  # noqa: F401
 from .graph import (GraphCSR, RobotGraph, batch, complete_edges, complete_graph, frame_graph,  # noqa: F401
                     graph, knn_edges, load_graphs, save_graphs, unbatch)

@@ -52,13 +52,12 @@ EXPORTED_SYMBOLS = (
     "mrp_edge_encoder_bwd_t_workspace",
     "mrp_edge_encoder_bwd_t",
     "mrp_frame_graph_build",
-    "mrp_gcn_fwd_fused_workspace_bytes",
-    "mrp_gcn_fwd_fused",
+    "mrp_stream_copy",
     "mrp_tuning_set",
     "mrp_abi_version",
     "mrp_error_string",
 )
-ABI_VERSION = 20
+ABI_VERSION = 21
 MAX_NODES = 16
 
 HIP_ERROR_NOT_SUPPORTED = 801  # hipErrorNotSupported: a fused path declines this shape
@@ -167,10 +166,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_edge_encoder_bwd.restype = ctypes.c_int
     lib.mrp_frame_graph_build.argtypes = [_P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]
     lib.mrp_frame_graph_build.restype = ctypes.c_int
-    lib.mrp_gcn_fwd_fused_workspace_bytes.argtypes = [_I32, _I32, _I32, _I32]
-    lib.mrp_gcn_fwd_fused_workspace_bytes.restype = ctypes.c_int64
-    lib.mrp_gcn_fwd_fused.argtypes = [_P, _I64, _P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _I64, _P, _I64, _P]
-    lib.mrp_gcn_fwd_fused.restype = ctypes.c_int
+    lib.mrp_stream_copy.argtypes = [_P, _P, _I64, _P]
+    lib.mrp_stream_copy.restype = ctypes.c_int
     lib.mrp_abi_version.argtypes = []
     lib.mrp_abi_version.restype = ctypes.c_int
     lib.mrp_error_string.argtypes = [ctypes.c_int]

@@ -13,7 +13,7 @@ SOURCES = [os.path.join(PKG_DIR, "csrc", f) for f in ("film_mean_fwd.hip", "film
                                                     "film_mean_bwd_9_12.hip", "film_mean_bwd_13_16.hip",
                                                     "edge_encoder.hip", "frame_graph.hip",
                                                     "compress_gemm.hip", "encoder_split.hip",
-                                                    "compress_split.hip", "gcn_fused.hip")]
+                                                    "compress_split.hip")]
 OBJ_DIR = os.path.join(PKG_DIR, "build")
 HEADERS = [os.path.join(REPO, "include", "mrp_gnn.h")] + [os.path.join(PKG_DIR, "csrc", h) for h in (
     "film_mean_kernels.hpp", "film_mean_bwd_launch.hpp", "fast_math.hpp", "tuning.hpp", "encoder_split.hpp")]
@@ -50,12 +50,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mcode-object-version=5", "-ffp-contract
 # per-source extras: the compress GEMMs' only VALU beside the MFMAs is the bias-row sum of the
 # weight gradient, where packed f32 ops (SLP-vectorised scalar adds) cost more than scalar ones
 # (MI355X_MICROARCH.md, filler prices)
-EXTRA_FLAGS = {"compress_gemm.hip": ["-fno-slp-vectorize"],
-               # the one-launch GCN layer: no packed-fp32 VALU beside the producers' MFMAs.  A build
-               # with SLP-vectorised (v_pk_*_f32) aggregation arithmetic returned wrong low halves of
-               # packed pairs in lanes 48-63 whenever matrix-core waves shared the SIMD (bit-exact
-               # without them; tools/diag_fused3.py, tools/lab_patches/r06_fused_old_build.py)
-               "gcn_fused.hip": ["-fno-slp-vectorize"]}
+EXTRA_FLAGS = {"compress_gemm.hip": ["-fno-slp-vectorize"]}
 
 
 def _compile(src: str, verbose: bool) -> str:

@@ -1,6 +1,6 @@
 #pragma once
 // encoder_split.hpp — the split-bf16 arithmetic and packed weight image of the edge encoder
-// (encoder_split.hip), shared with the fused encoder + aggregation launch (gcn_fused.hip).
+// (encoder_split.hip), kept apart from its kernels so kernel-lab variants can include them.
 //
 // Reference (xjh19971/multi-robot-perception-gnn-1, dgl/model/models.py:146-149):
 //     z = Linear(C, 2C)(ReLU(Linear(9, C)(pose)))          pose (E, 9) -> z (E, 2C)

@@ -63,6 +63,15 @@ hipError_t dispatch_fwd(int nt, bool complete, const AggArgs& a, const Geometry&
 
 }  // namespace
 
+// The streaming yardstick beside the aggregation rooflines (mrp_stream_copy): one nontemporal 16-byte
+// load and store per thread per trip, grid-stride, 256 threads, one trip per thread where the grid
+// allows (tools/copy_ceiling.hip's copy1, the best of round 1's copy sweep).
+__global__ void __launch_bounds__(256) stream_copy(const mrp::f4* __restrict__ in, mrp::f4* __restrict__ out,
+                                                   size_t n) {
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(in + i), out + i);
+}
+
 namespace mrp_host {
 Tuning& tuning() {
   static Tuning t;
@@ -72,7 +81,7 @@ Tuning& tuning() {
 
 extern "C" {
 
-int mrp_abi_version(void) { return 20; }
+int mrp_abi_version(void) { return 21; }
 
 int mrp_tuning_set(const char* name, int32_t value) {
   if (name == nullptr) return hipErrorInvalidValue;
@@ -112,8 +121,6 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"enc_bwd_psa", &t.enc_bwd_psa, 0, 2},
       {"enc_s1", &t.enc_s1, 0, 64},
       {"enc_s2", &t.enc_s2, 0, 64},
-      {"fused_producers", &t.fused_producers, 0, 4096},
-      {"fused_lab", &t.fused_lab, 0, 127},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(name, k.name) == 0) {
@@ -131,6 +138,17 @@ int mrp_tuning_set(const char* name, int32_t value) {
 }
 
 const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
+
+int mrp_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
+  if (bytes < 0 || (bytes % 16) != 0) return hipErrorInvalidValue;
+  if (bytes == 0) return hipSuccess;
+  if (!src || !dst || !aligned16(src) || !aligned16(dst)) return hipErrorInvalidValue;
+  const size_t n = (size_t)bytes / 16;
+  const size_t blocks = std::min<size_t>((n + 255) / 256, (size_t)1 << 30);
+  hipLaunchKernelGGL(stream_copy, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const mrp::f4*>(src), static_cast<mrp::f4*>(dst), n);
+  return hipGetLastError();
+}
 
 }  // extern "C"
 

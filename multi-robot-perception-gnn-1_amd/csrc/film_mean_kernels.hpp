@@ -360,24 +360,13 @@ struct CompleteSlots {
   static constexpr int kPer = (kMaxChanPerBlock * kSlots + kBlock - 1) / kBlock;  // max slots per thread
 };
 
-// One 8-byte gamma/beta pair read with an agent-scope load (global_load_dwordx2 sc1: past this CU's L1),
-// for pairs another workgroup of the same launch wrote (gcn_fused.hip's hand-off).
-// Uniform base + 32-bit byte offset (the fused launcher checks that E x 2C floats fit 2^31 bytes).
-__device__ __forceinline__ float2 load_gb_sc1(const float* base, uint32_t off) {
-  typedef __attribute__((address_space(1))) unsigned long long gu64;
-  const unsigned long long v = __hip_atomic_load(
-      (gu64*)(reinterpret_cast<const char*>(base) + off), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return __builtin_bit_cast(float2, v);
-}
-
-template <int NT, bool TR, bool SC1 = false>
-__device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, int c0, int base, float2* reg,
-                                               unsigned tid = threadIdx.x) {
+template <int NT, bool TR>
+__device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, int c0, int base, float2* reg) {
   constexpr int S = CompleteSlots<NT>::kSlots;
   const int tot = a.cpb * S;
 #pragma unroll
   for (int r = 0; r < CompleteSlots<NT>::kPer; ++r) {
-    const int t = base + (int)tid + r * blockDim.x;
+    const int t = base + threadIdx.x + r * blockDim.x;
     float2 val = make_float2(0.f, 0.f);
     if (t < tot) {
       int cl, v, u;
@@ -389,8 +378,7 @@ __device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, 
         } else {
           // raw value: the sigmoid (logits) is applied in complete_store, so the caller's feature
           // loads issue before this load has to return
-          const int64_t k = complete_eid(ebase, NT, u, v) * a.C + c;
-          val = SC1 ? load_gb_sc1(a.gb, (uint32_t)k * 8u) : *reinterpret_cast<const float2*>(a.gb + k * 2);
+          val = *reinterpret_cast<const float2*>(a.gb + (complete_eid(ebase, NT, u, v) * a.C + c) * 2);
         }
       }
     }
@@ -400,7 +388,7 @@ __device__ __forceinline__ void complete_fetch(const AggArgs& a, int64_t ebase, 
 
 template <int NT, bool BWD>
 __device__ __forceinline__ void complete_store(const AggArgs& a, int base, const float2* reg, float* Ga, float* Gb,
-                                               float2* Sg = nullptr, unsigned tid = threadIdx.x) {
+                                               float2* Sg = nullptr) {
   constexpr int S = CompleteSlots<NT>::kSlots;
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
@@ -410,7 +398,7 @@ __device__ __forceinline__ void complete_store(const AggArgs& a, int base, const
   const bool act = a.logits && a.mode != MRP_AGG_COPY_MEAN;
 #pragma unroll
   for (int r = 0; r < CompleteSlots<NT>::kPer; ++r) {
-    const int t = base + (int)tid + r * blockDim.x;
+    const int t = base + threadIdx.x + r * blockDim.x;
     if (t < tot) {
       int cl, v, u;
       complete_slot<NT, BWD>(a, t, cl, v, u);
@@ -430,14 +418,14 @@ __device__ __forceinline__ void complete_store(const AggArgs& a, int base, const
 }
 
 // Remaining slot chunks (only when a small workgroup owns more than kPer slots per thread).
-template <int NT, bool BWD, bool SC1 = false>
+template <int NT, bool BWD>
 __device__ __forceinline__ void complete_rest(const AggArgs& a, int64_t ebase, int c0, float* Ga, float* Gb,
-                                              float2* Sg = nullptr, unsigned tid = threadIdx.x) {
+                                              float2* Sg = nullptr) {
   const int chunk = CompleteSlots<NT>::kPer * blockDim.x;
   for (int base = chunk; base < a.cpb * CompleteSlots<NT>::kSlots; base += chunk) {
     float2 reg[CompleteSlots<NT>::kPer];
-    complete_fetch<NT, BWD, SC1>(a, ebase, c0, base, reg, tid);
-    complete_store<NT, BWD>(a, base, reg, Ga, Gb, Sg, tid);
+    complete_fetch<NT, BWD>(a, ebase, c0, base, reg);
+    complete_store<NT, BWD>(a, base, reg, Ga, Gb, Sg);
   }
 }
 
@@ -447,23 +435,8 @@ __device__ __forceinline__ void complete_rest(const AggArgs& a, int64_t ebase, i
 // MODE >= 0: the FiLM mode as a compile-time constant (the hot path: COMPLETE, MRP_AGG_FILM_MEAN,
 // N <= 8): no per-term select between the modes, and the mean's division by N - 1 as the exact
 // three-instruction quotient (fast_math.hpp) for a whole slice at once.  MODE = -1: mode at run time.
-// The gamma/beta rows are ready when the launch starts (every launch but the fused one).
-struct NoHandoff {
-  static constexpr bool kFused = false;
-  __device__ void issue(int, int) {}
-  __device__ bool wait() { return true; }
-  __device__ bool all_ready(bool) { return true; }
-};
-
-// blk: the workgroup's index in the aggregation grid.  Hook: NoHandoff, or the fused launch's
-// hand-off (gcn_fused.hip) — issue() requests the readiness words of graph b's gamma/beta rows before
-// the first slice's loads, wait() spins (bounded) until this wave sees them ready, all_ready() makes
-// that workgroup-uniform (false: the body returns false at once and its caller produces the rows), and
-// the rows are read past L1 (agent-scope loads).  Returns true once the workgroup's output is written.
-// tid: the thread's index (threadIdx.x; the fused launch's second pass passes a copy the compiler cannot
-// relate to the first pass's, so no index arithmetic stays live across the producer routine between them).
-template <int NT, int VEC, bool COMPLETE, int MODE, class Hook>
-__device__ __forceinline__ bool film_fwd_body(const AggArgs& a, unsigned blk, Hook& hook, unsigned tid = threadIdx.x) {
+template <int NT, int VEC, bool COMPLETE, int MODE = -1>
+__global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
   constexpr int SZ = Tile<NT>::SZ;
   constexpr int NTP = Tile<NT>::NTP;
   constexpr bool kBatchDiv = COMPLETE && MODE == MRP_AGG_FILM_MEAN && NT >= 2;
@@ -479,8 +452,8 @@ __device__ __forceinline__ bool film_fwd_body(const AggArgs& a, unsigned blk, Ho
   // grid-stride copy (178 vs 210 us at the bench size, tools/fwd_lab.hip), and the prologue they
   // repeat is a few KiB of gamma/beta from L2.
   const int ps = a.psplit > 1 ? a.psplit : 1;
-  const int item = blk / ps;
-  const int seg = blk - item * ps;
+  const int item = blockIdx.x / ps;
+  const int seg = blockIdx.x - item * ps;
   const int b = item / a.ncb;
   const int cb = item - b * a.ncb;
   const int seglen = (a.PV + ps - 1) / ps;
@@ -488,11 +461,11 @@ __device__ __forceinline__ bool film_fwd_body(const AggArgs& a, unsigned blk, Ho
   const int jend = min(a.PV, jbeg + seglen);
   const int node0 = COMPLETE ? b * NT : a.goff[b];
   const int n = COMPLETE ? NT : min(a.goff[b + 1] - node0, NT);
-  if (n <= 0) return true;  // whole workgroup: empty graph
+  if (n <= 0) return;  // whole workgroup: empty graph
   const int c0 = cb * a.cpb;
 
-  const int grp = tid / a.lpc;
-  const int li = tid - grp * a.lpc;
+  const int grp = threadIdx.x / a.lpc;
+  const int li = threadIdx.x - grp * a.lpc;
   const int c = c0 + grp;
   const bool active = grp < a.cpb && c < a.C;
   // uniform per-graph/channel-block bases, per-lane 32-bit byte offsets (see at_bytes)
@@ -500,13 +473,10 @@ __device__ __forceinline__ bool film_fwd_body(const AggArgs& a, unsigned blk, Ho
   float* ob = a.out + (int64_t)node0 * a.os + (int64_t)c0 * a.P;
   const uint32_t lane_plane = (uint32_t)grp * (uint32_t)a.P * 4u;
 
-  // prologue part 1 (COMPLETE): gamma/beta into registers (fused launch: the readiness words first)
+  // prologue part 1 (COMPLETE): gamma/beta into registers
   float2 reg[CompleteSlots<NT>::kPer];
   const int64_t ebase = (int64_t)b * NT * (NT - 1);
-  if constexpr (Hook::kFused)
-    hook.issue(b, c0);
-  else if (COMPLETE)
-    complete_fetch<NT, false>(a, ebase, c0, 0, reg, tid);
+  if (COMPLETE) complete_fetch<NT, false>(a, ebase, c0, 0, reg);
   // first slice of the sweep, issued before the weight tiles are needed
   int j = jbeg + li;
   // element k of every source's slice in one NT-wide vector value: when the compiler keeps a
@@ -524,22 +494,14 @@ __device__ __forceinline__ bool film_fwd_body(const AggArgs& a, unsigned blk, Ho
     }
   };
   if (active && j < jend) load_slice(j);
-  if constexpr (Hook::kFused) {
-    static_assert(COMPLETE, "the fused hand-off serves complete graphs");
-    const bool ready = hook.wait();  // this wave: graph b's rows published (bounded spin)
-    // a wave gave up waiting: the whole workgroup returns false before using anything (its caller
-    // produces the missing rows and runs the body again)
-    if (!hook.all_ready(ready)) return false;
-    complete_fetch<NT, false, true>(a, ebase, c0, 0, reg, tid);
-  }
   // prologue part 2: tiles into LDS
   if (COMPLETE) {
-    complete_store<NT, false>(a, 0, reg, Ga, Gb, nullptr, tid);
-    complete_rest<NT, false, Hook::kFused>(a, ebase, c0, Ga, Gb, nullptr, tid);
+    complete_store<NT, false>(a, 0, reg, Ga, Gb);
+    complete_rest<NT, false>(a, ebase, c0, Ga, Gb);
   } else
     build_tiles_csr<NT, false>(a, node0, n, c0, Ga, Gb, degf, emask);
   __syncthreads();
-  if (!active) return true;
+  if (!active) return;
 
   const bool film = MODE >= 0 ? MODE != MRP_AGG_COPY_MEAN : a.mode != MRP_AGG_COPY_MEAN;
   const bool mean = MODE >= 0 ? MODE != MRP_AGG_FILM_SUM : a.mode != MRP_AGG_FILM_SUM;
@@ -668,13 +630,6 @@ __device__ __forceinline__ bool film_fwd_body(const AggArgs& a, unsigned blk, Ho
     j += a.lpc;
     if (j < jend) load_slice(j);
   }
-  return true;
-}
-
-template <int NT, int VEC, bool COMPLETE, int MODE = -1>
-__global__ void __launch_bounds__(kBlock) film_fwd(AggArgs a) {
-  NoHandoff h;
-  film_fwd_body<NT, VEC, COMPLETE, MODE>(a, blockIdx.x, h);
 }
 
 // ---------------------------------------------------------------------------

@@ -53,14 +53,6 @@ struct Tuning {
   // pre-split (W2^T's image; dz^T written as an image by dzT_pack), 1 = only W2^T's, 0 = neither
   int enc_bwd_psa = 2;
   int enc_s1 = 0, enc_s2 = 0;  // mrp_edge_encoder_bwd_fused: split counts of its two products (0: planner)
-  // mrp_gcn_fwd_fused (gcn_fused.hip): producer workgroups computing the encoder's logits beside the
-  // aggregation (at most one CAS round of 64 items each)
-  int fused_producers = 128;
-  // lab bits (0 in the product): 1 = the launcher skips its memset (the caller zeroes the words),
-  // 2 = aggregation workgroups do not wait (rows assumed present: prologue-cost A/B only),
-  // 4 = producers return at once (with 2: the aggregation alone in the fused grid), 8 = producers
-  // store nothing, 16 = producers skip the MFMAs, 32 = producers only sleep, 64 = timeline (gcn_fused.hip)
-  int fused_lab = 0;
 };
 Tuning& tuning();
 

@@ -64,10 +64,6 @@ def set_logits_path(path: str) -> None:
     _LOGITS_PATH = path
 
 
-def logits_path() -> str:
-    return _LOGITS_PATH
-
-
 # packed split-bf16 weight images, per second-Linear module: (key, tensor).  The key holds the data
 # pointers and autograd versions of W1, b1, W2: an optimizer step (an in-place update under no_grad)
 # bumps a version and the image is rebuilt on the next call.  Writes through ``.data`` bypass the

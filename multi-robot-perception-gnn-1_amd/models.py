@@ -35,16 +35,7 @@ import torch.nn as nn
 
 from .aggregate import film_mean, film_mean_cat, film_mean_mix, film_mean_residual
 from .compress import compress_1x1, compress_path, film_compress, film_compress_supported
-from .encoder import edge_logits, logits_path
-from .fused import gcn_forward_fused
-
-
-def fused_forward(enc: "edge_encoder", x: torch.Tensor, pose: torch.Tensor, csr) -> "torch.Tensor | None":
-    """The one-launch no-grad layer (``fused.gcn_forward_fused``) when the encoder runs on the split
-    path (the default); None otherwise or when the shape is not one it serves."""
-    if logits_path() != "split":
-        return None
-    return gcn_forward_fused(x, pose, csr, enc.layers[0], enc.layers[2])
+from .encoder import edge_logits
 
 
 def clear_packed_weights() -> None:
@@ -151,15 +142,8 @@ class GCN(_PackedImages, nn.Module):
         mode = _opt(self.opt, "gcn_mode", "film_mean")
         if mode == "copy_mean":
             return film_mean(x, None, g.csr(x.device), mode)
-        pose = g.edata["pose"]
-        if mode == "film_mean" and x.is_cuda and not (torch.is_grad_enabled() and (
-                x.requires_grad or pose.requires_grad or any(p.requires_grad for p in self.edge_encoder.parameters()))):
-            # no gradient wanted (the eval path): encoder + aggregation in one launch where it serves
-            out = fused_forward(self.edge_encoder, x, pose, g.csr(x.device))
-            if out is not None:
-                return out
         # logits in, sigmoid applied inside the aggregation kernel
-        z = self.edge_encoder.logits(pose)
+        z = self.edge_encoder.logits(g.edata["pose"])
         return film_mean(x, z, g.csr(x.device), mode, logits=True)
 
     def forward_cat(self, g, feats: torch.Tensor = None) -> torch.Tensor:

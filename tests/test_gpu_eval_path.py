@@ -1,9 +1,7 @@
 """The inference path end to end: what the reference's eval loop runs (``torch.no_grad()`` around
 ``model(data)``, ``dgl/eval.py:184-198``, ``dgl/training.py:225-240``) and what ``bench.py`` times —
-``GCN.forward`` with no gradient wanted, i.e. the split-bf16 edge encoder -> logits -> sigmoid inside the
-aggregation kernel -> the FiLM-mean sweep: one launch where ``mrp_gcn_fwd_fused`` serves the shape (the
-headline; bit-identical to the two launches, ``tests/test_gpu_fused.py``), else
-``mrp_edge_encoder_fwd_split`` then ``film_fwd``.
+``GCN.forward`` with no gradient wanted, i.e. the one-launch split-bf16 edge encoder
+(``mrp_edge_encoder_fwd_split``) -> logits -> sigmoid inside the aggregation kernel -> ``film_fwd``.
 
 * against the reference's own golden fixture (its ``GCN``/``edge_encoder`` modules, stub-imported by
   ``tests/golden/make_golden.py``) at 1e-5, the north-star tolerance;
@@ -13,7 +11,7 @@ headline; bit-identical to the two launches, ``tests/test_gpu_fused.py``), else
   that exposed a biased single-accumulator sum in the compress GEMMs;
 * the train (autograd: hidden kernel + fp32-MFMA logits) and eval (split-bf16) encoders on the same
   weights: both within the yardstick, and their mutual difference stated.
-Every test asserts which encoder kernel actually ran (``encoder.PATH_COUNTS``)."""
+Every test asserts the split kernel actually ran (``encoder.PATH_COUNTS``)."""
 import types
 
 import numpy as np
@@ -76,11 +74,11 @@ def test_eval_headline_vs_float64(cuda_device):
     torch.manual_seed(0)
     gcn = m.GCN(types.SimpleNamespace(feature_dim=C)).to(cuda_device)
     x = g.ndata["image"]
-    before = m.encoder.PATH_COUNTS["fused"]
+    before = _split_calls()
     with torch.no_grad():
         out = gcn(g, x)
     torch.cuda.synchronize()
-    assert m.encoder.PATH_COUNTS["fused"] == before + 1  # the one-launch layer (tests/test_gpu_fused.py)
+    assert _split_calls() == before + 1
     params = {"enc." + k: v.detach() for k, v in gcn.edge_encoder.named_parameters()}
     src, dst = (t.to(cuda_device).long() for t in g.edges())
     pose = g.edata["pose"]
