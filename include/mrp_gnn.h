@@ -352,8 +352,14 @@ int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const floa
  *                                      for the dW2 product too (same products, same order: dW1, db1 and
  *                                      dW2 bit-identical to the split form; db2 summed per 64-edge block);
  *                                      workspace: _fused_workspace(E, C) bytes
+ *   mrp_edge_encoder_bwd_pose          the pose gradient (the encoder's input, wanted only when poses
+ *                                      require grad): dpose (E, 9) = dpre^T W1 with dpre as for _bwd_t;
+ *                                      any E, C; workspace: _pose_workspace(E, C) bytes (0: none needed)
  * Requirements of _bwd_split and _bwd_fused (else hipErrorNotSupported): E % 32 == 0, C % 32 == 0,
- * 16-byte aligned operands.  All sums in a fixed order: deterministic.
+ * 16-byte aligned operands.  Shapes outside them run the same kernels on zero-padded operands
+ * (encoder.py, EdgeEncoderPaddedFunction: E and C rounded up to 32, zero weight rows and columns, zero
+ * gradient rows — every padded term a product with an exact zero).  All sums in a fixed order:
+ * deterministic.
  */
 int mrp_edge_encoder_fwd_split_train(const float* pose, const void* packed, const float* b2, int32_t num_edges,
                                      int32_t C, float* z, float* hT, int64_t hT_stride, void* stream);
@@ -371,6 +377,10 @@ int64_t mrp_edge_encoder_bwd_t_workspace(int32_t num_edges, int32_t C);
 int mrp_edge_encoder_bwd_t(const float* dhT, int64_t dhT_stride, const float* hT, int64_t hT_stride,
                            const float* pose, int32_t num_edges, int32_t C, float* dw1, float* db1, void* workspace,
                            int64_t workspace_bytes, void* stream);
+int64_t mrp_edge_encoder_bwd_pose_workspace(int32_t num_edges, int32_t C);
+int mrp_edge_encoder_bwd_pose(const float* dhT, int64_t dhT_stride, const float* hT, int64_t hT_stride,
+                              const float* w1, int32_t num_edges, int32_t C, float* dpose, void* workspace,
+                              int64_t workspace_bytes, void* stream);
 
 /*
  * Backward of the edge encoder's reductions (dgl/model/models.py:147-149), run after the two
@@ -433,7 +443,8 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 21 = this header: v19 plus
- * the streaming yardstick mrp_stream_copy; 20: v19 plus a one-launch no-grad GCN layer
+ * the streaming yardstick mrp_stream_copy and the encoder's pose gradient (mrp_edge_encoder_bwd_pose
+ * + workspace); 20: v19 plus a one-launch no-grad GCN layer
  * (mrp_gcn_fwd_fused), measured slower than the two launches it replaced and removed in 21
  * (tools/lab_patches/r06_fused_layer.patch); 19: v18 with
  * mrp_edge_encoder_bwd_fused taking W2^T's packed image (w2T_packed); 18: v17 without

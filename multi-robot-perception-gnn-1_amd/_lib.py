@@ -51,6 +51,8 @@ EXPORTED_SYMBOLS = (
     "mrp_edge_encoder_bwd_fused",
     "mrp_edge_encoder_bwd_t_workspace",
     "mrp_edge_encoder_bwd_t",
+    "mrp_edge_encoder_bwd_pose_workspace",
+    "mrp_edge_encoder_bwd_pose",
     "mrp_frame_graph_build",
     "mrp_stream_copy",
     "mrp_tuning_set",
@@ -160,6 +162,10 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_edge_encoder_bwd_t_workspace.restype = ctypes.c_int64
     lib.mrp_edge_encoder_bwd_t.argtypes = [_P, _I64, _P, _I64, _P, _I32, _I32, _P, _P, _P, _I64, _P]
     lib.mrp_edge_encoder_bwd_t.restype = ctypes.c_int
+    lib.mrp_edge_encoder_bwd_pose_workspace.argtypes = [_I32, _I32]
+    lib.mrp_edge_encoder_bwd_pose_workspace.restype = ctypes.c_int64
+    lib.mrp_edge_encoder_bwd_pose.argtypes = [_P, _I64, _P, _I64, _P, _I32, _I32, _P, _P, _I64, _P]
+    lib.mrp_edge_encoder_bwd_pose.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_workspace.argtypes = [_I32, _I32]
     lib.mrp_edge_encoder_bwd_workspace.restype = ctypes.c_int64
     lib.mrp_edge_encoder_bwd.argtypes = [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P]

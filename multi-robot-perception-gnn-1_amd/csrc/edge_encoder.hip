@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "mrp_gnn.h"
 
 namespace mrp_enc {
@@ -299,7 +301,97 @@ __global__ void __launch_bounds__(256) encoder_bwd_t_final(const float* __restri
   }
 }
 
+// dpose[e][i] = sum_k dpre[k][e] w1[k][i] (the pose gradient, models.py:146's input; K = C, 9 outputs per
+// edge).  Block (64-edge block, k slice s): wave w walks k = k0 + w, k0 + w + 4, ... of the slice, one
+// edge per lane (dh^T / h^T rows read 64 floats at a time, coalesced; w1's row uniform across the wave);
+// the 4 waves' sums meet in LDS in wave order, then either straight into dpose (one slice) or into
+// part[s][e][9], summed over the slices in order by encoder_bwd_pose_final: deterministic.
+__global__ void __launch_bounds__(256) encoder_bwd_pose(const float* __restrict__ dhT, int64_t dhs,
+                                                        const float* __restrict__ hT, int64_t hs,
+                                                        const float* __restrict__ w1, int E, int C, int kslice,
+                                                        float* __restrict__ out) {
+  __shared__ float red[4][64][NIN];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  const int k0 = blockIdx.y * kslice, k1 = min(C, k0 + kslice);
+  float acc[NIN];
+#pragma unroll
+  for (int i = 0; i < NIN; ++i) acc[i] = 0.f;
+  if (e < E) {
+#pragma unroll 4
+    for (int k = k0 + w; k < k1; k += 4) {
+      const float h = hT[(int64_t)k * hs + e], g = dhT[(int64_t)k * dhs + e];
+      const float d = h > 0.f ? g : 0.f;
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) acc[i] = fmaf(d, w1[k * NIN + i], acc[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NIN; ++i) red[w][lane][i] = acc[i];
+  __syncthreads();
+  for (int t = threadIdx.x; t < 64 * NIN; t += 256) {
+    const int el = t / NIN, i = t - el * NIN, ee = blockIdx.x * 64 + el;
+    if (ee < E)
+      out[((int64_t)blockIdx.y * E + ee) * NIN + i] = ((red[0][el][i] + red[1][el][i]) + red[2][el][i]) + red[3][el][i];
+  }
+}
+
+__global__ void __launch_bounds__(256) encoder_bwd_pose_final(const float* __restrict__ part, int ns, int64_t n,
+                                                              float* __restrict__ dpose) {
+  const int64_t t = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (t >= n) return;
+  float s = part[t];
+  for (int b = 1; b < ns; ++b) s += part[(int64_t)b * n + t];
+  dpose[t] = s;
+}
+
+// k slices of encoder_bwd_pose: enough blocks to cover the chip (>= 1024 with 64-edge blocks), each
+// wave keeping >= 16 k terms; a multiple of 4 so every wave's k walk starts on its own residue
+inline int pose_slices(int E, int C, int* kslice) {
+  const int neb = (E + 63) / 64;
+  int s = (1024 + neb - 1) / neb;
+  s = std::max(1, std::min(s, C / 64));
+  int ks = (C + s - 1) / s;
+  ks = (ks + 3) / 4 * 4;
+  s = (C + ks - 1) / ks;
+  *kslice = ks;
+  return s;
+}
+
 }  // namespace mrp_enc
+
+extern "C" int64_t mrp_edge_encoder_bwd_pose_workspace(int32_t num_edges, int32_t C) {
+  if (num_edges <= 0 || C <= 0) return 0;
+  int ks;
+  const int s = mrp_enc::pose_slices(num_edges, C, &ks);
+  return s > 1 ? (int64_t)s * num_edges * mrp_enc::NIN * 4 : 0;
+}
+
+extern "C" int mrp_edge_encoder_bwd_pose(const float* dhT, int64_t dhT_stride, const float* hT, int64_t hT_stride,
+                                         const float* w1, int32_t num_edges, int32_t C, float* dpose,
+                                         void* workspace, int64_t workspace_bytes, void* stream) {
+  if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
+  if (num_edges == 0) return hipSuccess;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!dpose) return hipErrorInvalidValue;
+  if (C == 0) return hipMemsetAsync(dpose, 0, (size_t)num_edges * mrp_enc::NIN * 4, st);
+  if (!dhT || !hT || !w1 || dhT_stride < num_edges || hT_stride < num_edges ||
+      (int64_t)C * mrp_enc::NIN >= ((int64_t)1 << 31))
+    return hipErrorInvalidValue;
+  int ks;
+  const int s = mrp_enc::pose_slices(num_edges, C, &ks);
+  if (s > 1 && (!workspace || workspace_bytes < mrp_edge_encoder_bwd_pose_workspace(num_edges, C)))
+    return hipErrorInvalidValue;
+  float* out = s > 1 ? static_cast<float*>(workspace) : dpose;
+  hipLaunchKernelGGL(mrp_enc::encoder_bwd_pose, dim3((num_edges + 63) / 64, s), dim3(256), 0, st, dhT, dhT_stride,
+                     hT, hT_stride, w1, num_edges, C, ks, out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || s == 1) return e;
+  const int64_t n = (int64_t)num_edges * mrp_enc::NIN;
+  hipLaunchKernelGGL(mrp_enc::encoder_bwd_pose_final, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, s, n,
+                     dpose);
+  return hipGetLastError();
+}
 
 extern "C" int mrp_edge_encoder_bwd_prep(const float* dz, int32_t num_edges, int32_t C, float* dzT,
                                          int64_t dzT_stride, void* stream) {

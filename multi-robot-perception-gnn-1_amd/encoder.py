@@ -11,12 +11,15 @@ once per weight version (:func:`packed_weights`):
 * training (:class:`EdgeEncoderSplitFunction`, E % 32 == 0 and C % 32 == 0 — every reference
   configuration): the same kernel also writes h^T for the backward; the backward's two GEMMs
   (``dh^T = W2^T dz^T``, ``dW2 = dz^T h`` with db2) run on the split-bf16 weight-gradient kernel of
-  ``compress_split.hip`` on two streams, the ReLU mask, dW1 and db1 in one HIP pass.
+  ``compress_split.hip`` (one launch of both, or two streams), the ReLU mask, dW1 and db1 in one HIP
+  pass, the pose gradient (when poses require grad) on ``mrp_edge_encoder_bwd_pose``;
+* any other E or C (:class:`EdgeEncoderPaddedFunction`, and inference with C % 32 != 0): the same
+  kernels on operands zero-padded to multiples of 32 (:func:`padded_weights`) — every padded term a
+  product with an exact zero, so z and the gradients are the leading blocks of the padded results.
 
-Other shapes train through :class:`EdgeEncoderFunction`: ``mrp_edge_hidden_fwd`` (K = 9, a streaming
-write) + ``mrp_edge_logits_fwd`` (fp32 MFMA, 64 x 64 tiles, bias in the epilogue; C % 32 != 0 or
-``set_logits_path("library")``: ``torch.addmm``), the backward GEMMs on torch (two streams) and the
-small reductions in one HIP pass (``mrp_edge_encoder_bwd``).
+:class:`EdgeEncoderFunction` (``mrp_edge_hidden_fwd`` + ``mrp_edge_logits_fwd`` in fp32, the backward
+GEMMs on torch) serves only the comparison paths (``set_logits_path("hip" | "library")``) and shapes
+past the split kernels' 32-bit offsets (E x 2C >= 2^29 floats after padding).
 """
 from __future__ import annotations
 
@@ -76,15 +79,10 @@ def clear_packed_weights() -> None:
     _packed.clear()
     _w2t_cache.clear()
     _w2t_img_cache.clear()
+    _padded.clear()
 
 
-def packed_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> torch.Tensor:
-    """The ``mrp_edge_encoder_pack`` image of (W1, b1, W2), rebuilt when a weight changed."""
-    w1, b1, w2 = l1.weight, l1.bias, l2.weight
-    key = tuple((t.data_ptr(), t._version, t.device.index) for t in (w1, b1, w2))
-    hit = _packed.get(l2)
-    if hit is not None and hit[0] == key:
-        return hit[1]
+def _pack(w1, b1, w2) -> torch.Tensor:
     C = w1.shape[0]
     lib = _lib.load_library()
     nbytes = int(lib.mrp_edge_encoder_pack_bytes(C))
@@ -94,32 +92,51 @@ def packed_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> torch.Tensor:
         _lib.check(lib.mrp_edge_encoder_pack(_ptr(w1c), _ptr(b1c), _ptr(w2c), C, _ptr(img),
                                              ctypes.c_void_p(torch.cuda.current_stream(w1.device).cuda_stream)),
                    "mrp_edge_encoder_pack")
+    return img
+
+
+def packed_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> torch.Tensor:
+    """The ``mrp_edge_encoder_pack`` image of (W1, b1, W2), rebuilt when a weight changed."""
+    w1, b1, w2 = l1.weight, l1.bias, l2.weight
+    key = tuple((t.data_ptr(), t._version, t.device.index) for t in (w1, b1, w2))
+    hit = _packed.get(l2)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    img = _pack(w1, b1, w2)
     _packed[l2] = (key, img)
     return img
 
 
 def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
     """z = relu(pose W1^T + b1) W2^T + b2, (E, 2C), in one launch on the split-bf16 matrix cores
-    (``mrp_edge_encoder_fwd_split``); None when the kernel declines the shape (C % 32 != 0)."""
+    (``mrp_edge_encoder_fwd_split``); C % 32 != 0 runs on the zero-padded weights
+    (:func:`padded_weights`) and keeps z's 2C leading columns.  None when no weight image exists for
+    the shape (C beyond ``mrp_edge_encoder_pack``'s bound, layers not the reference's)."""
     C = l1.weight.shape[0]
     if not pose.is_cuda:
         raise RuntimeError("mrp_gnn: the edge encoder kernel runs only on the GPU; no CPU fallback")
-    if C % 32 != 0 or tuple(l1.weight.shape) != (C, 9) or tuple(l2.weight.shape) != (2 * C, C) \
-            or l1.bias is None or not image_supported(C):
+    if tuple(l1.weight.shape) != (C, 9) or tuple(l2.weight.shape) != (2 * C, C) or l1.bias is None or C == 0:
         return None
-    img = packed_weights(l1, l2)
+    if C % 32 == 0 and image_supported(C):
+        img = packed_weights(l1, l2)
+        b2 = l2.bias.detach().contiguous().float() if l2.bias is not None else None
+        Cp = C
+    elif image_supported(_pad32(C)):
+        rec = padded_weights(l1, l2)
+        img, b2, Cp = rec.img, rec.b2, rec.Cp
+    else:
+        return None
     pose = pose.detach().contiguous().float()
-    b2 = l2.bias.detach().contiguous().float() if l2.bias is not None else None
     E = pose.shape[0]
-    z = torch.empty((E, 2 * C), device=pose.device, dtype=torch.float32)
+    z = torch.empty((E, 2 * Cp), device=pose.device, dtype=torch.float32)
     lib = _lib.load_library()
     with torch.cuda.device(pose.device):
-        code = lib.mrp_edge_encoder_fwd_split(_ptr(pose), _ptr(img), _ptr(b2) if b2 is not None else None, E, C,
+        code = lib.mrp_edge_encoder_fwd_split(_ptr(pose), _ptr(img), _ptr(b2) if b2 is not None else None, E, Cp,
                                               _ptr(z), ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream))
     if code == _lib.HIP_ERROR_NOT_SUPPORTED:
         return None
     _lib.check(code, "mrp_edge_encoder_fwd_split")
-    return z
+    return z if Cp == C else z[:, : 2 * C].contiguous()
 
 
 def logits_forward(h, w2, b2) -> torch.Tensor:
@@ -139,23 +156,6 @@ def logits_forward(h, w2, b2) -> torch.Tensor:
                                        ctypes.c_void_p(torch.cuda.current_stream(h.device).cuda_stream))
     _lib.check(code, "mrp_edge_logits_fwd")
     return z
-
-
-class EdgeHiddenFunction(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, pose, w1, b1):
-        h = hidden_forward(pose, w1, b1)
-        ctx.save_for_backward(pose, w1, h)
-        return h
-
-    @staticmethod
-    def backward(ctx, gh):
-        pose, w1, h = ctx.saved_tensors
-        dpre = gh * (h > 0)
-        dw1 = dpre.t().mm(pose.float())
-        db1 = dpre.sum(0)
-        dpose = dpre.mm(w1) if ctx.needs_input_grad[0] else None
-        return dpose, dw1, db1
 
 
 _side_streams = {}
@@ -233,7 +233,8 @@ class EdgeEncoderFunction(torch.autograd.Function):
 
 
 #: calls per encoder path ("split": mrp_edge_encoder_fwd_split,
-#: "split_train": EdgeEncoderSplitFunction, "autograd": EdgeEncoderFunction) — lets tests assert which
+#: "split_train": EdgeEncoderSplitFunction, "split_padded": EdgeEncoderPaddedFunction,
+#: "autograd": EdgeEncoderFunction) — lets tests assert which
 #: kernels a forward actually ran
 PATH_COUNTS = collections.Counter()
 
@@ -264,14 +265,7 @@ def transposed_w2(l2: torch.nn.Linear) -> torch.Tensor:
     return t
 
 
-def packed_w2t(l2: torch.nn.Linear) -> torch.Tensor:
-    """W2^T's packed split-bf16 image (``mrp_compress_split_pack(w2, C, 1, C, 2C)``) — the dh^T product's
-    row operand in ``mrp_edge_encoder_bwd_fused`` — cached per weight version like :func:`transposed_w2`."""
-    w2 = l2.weight
-    key = (w2.data_ptr(), w2._version, w2.device.index)
-    hit = _w2t_img_cache.get(l2)
-    if hit is not None and hit[0] == key:
-        return hit[1]
+def _pack_w2t(w2: torch.Tensor) -> torch.Tensor:
     C = w2.shape[1]
     lib = _lib.load_library()
     nbytes = int(lib.mrp_compress_split_pack_bytes(C, 2 * C))
@@ -281,6 +275,18 @@ def packed_w2t(l2: torch.nn.Linear) -> torch.Tensor:
         _lib.check(lib.mrp_compress_split_pack(_ptr(w2c), C, 1, C, 2 * C, _ptr(img),
                                                ctypes.c_void_p(torch.cuda.current_stream(w2.device).cuda_stream)),
                    "mrp_compress_split_pack")
+    return img
+
+
+def packed_w2t(l2: torch.nn.Linear) -> torch.Tensor:
+    """W2^T's packed split-bf16 image (``mrp_compress_split_pack(w2, C, 1, C, 2C)``) — the dh^T product's
+    row operand in ``mrp_edge_encoder_bwd_fused`` — cached per weight version like :func:`transposed_w2`."""
+    w2 = l2.weight
+    key = (w2.data_ptr(), w2._version, w2.device.index)
+    hit = _w2t_img_cache.get(l2)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    img = _pack_w2t(w2)
     _w2t_img_cache[l2] = (key, img)
     return img
 
@@ -331,67 +337,201 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz):
         pose, w1, b1, w2, b2, hT = ctx.saved_tensors
-        need = ctx.needs_input_grad
-        dz = dz.contiguous().float()
-        E, C = pose.shape[0], w1.shape[0]
+        params = (None, w1, b1, w2, b2)
         dev = dz.device
-        cur = torch.cuda.current_stream(dev)
-        lib = _lib.load_library()
-        nbytes = int(lib.mrp_edge_encoder_bwd_split_workspace(E, C))
 
-        def workspace():
-            return torch.empty((nbytes + 3) // 4, device=dev) if nbytes > 0 else None
+        def out(i, shape):
+            return _grad_out(params[i], shape, dev)
+        return split_backward(dz.contiguous().float(), pose, hT, w1, ctx.needs_input_grad, out,
+                              lambda: transposed_w2(ctx.l2), lambda: packed_w2t(ctx.l2)) + (None, None)
 
-        if not need[0] and need[1] and need[2] and need[3] and need[4] and _BWD_FUSED:
-            # every parameter gradient, no pose gradient (the reference's case: poses are data): the
-            # three-launch single-stream form, dh^T never materialised
-            dw1, db1 = _grad_out(w1, (C, 9), dev), _grad_out(b1, (C,), dev)
-            dw2, db2 = _grad_out(w2, (2 * C, C), dev), _grad_out(b2, (2 * C,), dev)
-            wsf = torch.empty((int(lib.mrp_edge_encoder_bwd_fused_workspace(E, C)) + 3) // 4, device=dev)
-            with torch.cuda.device(dev):
-                w2t, w2t_img = transposed_w2(ctx.l2), packed_w2t(ctx.l2)
-                _lib.check(lib.mrp_edge_encoder_bwd_fused(
-                    _ptr(dz), _ptr(w2t), _ptr(w2t_img) if w2t_img is not None else None, _ptr(hT), _ptr(pose), E, C,
-                    _ptr(dw1), _ptr(db1), _ptr(dw2), _ptr(db2),
-                    _ptr(wsf), wsf.numel() * 4, ctypes.c_void_p(cur.cuda_stream)), "mrp_edge_encoder_bwd_fused")
-            return None, dw1, db1, dw2, db2, None, None
-        dw2 = db2 = side = None
+
+def pose_grad(dhT: torch.Tensor, hT: torch.Tensor, w1: torch.Tensor) -> torch.Tensor:
+    """dpose (E, 9) = (dh^T (.) [h^T > 0])^T W1 on ``mrp_edge_encoder_bwd_pose`` (h^T, dh^T: (C, E))."""
+    C, E = hT.shape
+    dev = hT.device
+    dpose = torch.empty((E, 9), device=dev)
+    lib = _lib.load_library()
+    nbytes = int(lib.mrp_edge_encoder_bwd_pose_workspace(E, C))
+    ws = torch.empty((nbytes + 3) // 4, device=dev) if nbytes > 0 else None
+    w1c = w1.detach().contiguous().float()
+    with torch.cuda.device(dev):
+        _lib.check(lib.mrp_edge_encoder_bwd_pose(
+            _ptr(dhT), dhT.stride(0), _ptr(hT), hT.stride(0), _ptr(w1c), E, C, _ptr(dpose),
+            _ptr(ws) if ws is not None else None, nbytes, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+            "mrp_edge_encoder_bwd_pose")
+    return dpose
+
+
+def split_backward(dz, pose, hT, w1, need, out, w2t_get, w2t_img_get):
+    """The split-bf16 backward of ``z = relu(pose W1^T + b1) W2^T + b2`` (E % 32 == 0, C % 32 == 0):
+    ``need`` = needs_input_grad of (pose, w1, b1, w2, b2); ``out(i, shape)`` the buffer of parameter
+    gradient i (1..4); ``w2t_get`` / ``w2t_img_get`` build W2^T and its packed image on demand.
+    Returns (dpose, dw1, db1, dw2, db2)."""
+    E, C = pose.shape[0], hT.shape[0]
+    dev = dz.device
+    cur = torch.cuda.current_stream(dev)
+    lib = _lib.load_library()
+    nbytes = int(lib.mrp_edge_encoder_bwd_split_workspace(E, C))
+
+    def workspace():
+        return torch.empty((nbytes + 3) // 4, device=dev) if nbytes > 0 else None
+
+    if not need[0] and need[1] and need[2] and need[3] and need[4] and _BWD_FUSED:
+        # every parameter gradient, no pose gradient (the reference's case: poses are data): the
+        # three-launch single-stream form, dh^T never materialised
+        dw1, db1 = out(1, (C, 9)), out(2, (C,))
+        dw2, db2 = out(3, (2 * C, C)), out(4, (2 * C,))
+        wsf = torch.empty((int(lib.mrp_edge_encoder_bwd_fused_workspace(E, C)) + 3) // 4, device=dev)
         with torch.cuda.device(dev):
-            if need[3] or need[4]:  # dz^T, then dW2 = dz^T h with db2 as its row sums, on the side stream
-                dw2 = _grad_out(w2, (2 * C, C), dev) if need[3] else torch.empty((2 * C, C), device=dev)
-                db2 = _grad_out(b2, (2 * C,), dev) if need[4] else None
-                dzT = torch.empty((2 * C, E), device=dev)
-                wsa = workspace()
-                side = _side_stream(dev)
-                side.wait_stream(cur)
-                ss = ctypes.c_void_p(side.cuda_stream)
-                _lib.check(lib.mrp_edge_encoder_bwd_prep(_ptr(dz), E, C, _ptr(dzT), E, ss), "mrp_edge_encoder_bwd_prep")
-                _lib.check(lib.mrp_edge_encoder_bwd_split(
-                    None, _ptr(dzT), None, _ptr(hT), E, C, None, _ptr(dw2), _ptr(db2) if db2 is not None else None,
-                    _ptr(wsa) if wsa is not None else None, nbytes, ss), "mrp_edge_encoder_bwd_split")
-                for t in (dz, hT, dzT, wsa, dw2, db2):
-                    if t is not None:
-                        t.record_stream(side)
-            dw1 = db1 = dhT = None
-            if need[0] or need[1] or need[2]:  # dh^T = W2^T dz^T, then the ReLU mask, dW1, db1
-                w2t = transposed_w2(ctx.l2)
-                st = ctypes.c_void_p(cur.cuda_stream)
-                dhT = torch.empty((C, E), device=dev)
-                wsb = workspace()
-                _lib.check(lib.mrp_edge_encoder_bwd_split(
-                    _ptr(dz), None, _ptr(w2t), None, E, C, _ptr(dhT), None, None,
-                    _ptr(wsb) if wsb is not None else None, nbytes, st), "mrp_edge_encoder_bwd_split")
-                if need[1] or need[2]:
-                    dw1 = _grad_out(w1, (C, 9), dev) if need[1] else None
-                    db1 = _grad_out(b1, (C,), dev) if need[2] else None
-                    wst = torch.empty(max(int(lib.mrp_edge_encoder_bwd_t_workspace(E, C)) // 4, 1), device=dev)
-                    _lib.check(lib.mrp_edge_encoder_bwd_t(
-                        _ptr(dhT), E, _ptr(hT), E, _ptr(pose), E, C, _ptr(dw1) if dw1 is not None else None,
-                        _ptr(db1) if db1 is not None else None, _ptr(wst), wst.numel() * 4, st), "mrp_edge_encoder_bwd_t")
-            if side is not None:
-                cur.wait_stream(side)
-        dpose = (dhT * (hT > 0)).t().mm(w1.float()) if need[0] else None
-        return dpose, dw1, db1, dw2 if need[3] else None, db2, None, None
+            w2t, w2t_img = w2t_get(), w2t_img_get()
+            _lib.check(lib.mrp_edge_encoder_bwd_fused(
+                _ptr(dz), _ptr(w2t), _ptr(w2t_img) if w2t_img is not None else None, _ptr(hT), _ptr(pose), E, C,
+                _ptr(dw1), _ptr(db1), _ptr(dw2), _ptr(db2),
+                _ptr(wsf), wsf.numel() * 4, ctypes.c_void_p(cur.cuda_stream)), "mrp_edge_encoder_bwd_fused")
+        return None, dw1, db1, dw2, db2
+    dw2 = db2 = side = None
+    with torch.cuda.device(dev):
+        if need[3] or need[4]:  # dz^T, then dW2 = dz^T h with db2 as its row sums, on the side stream
+            dw2 = out(3, (2 * C, C)) if need[3] else torch.empty((2 * C, C), device=dev)
+            db2 = out(4, (2 * C,)) if need[4] else None
+            dzT = torch.empty((2 * C, E), device=dev)
+            wsa = workspace()
+            side = _side_stream(dev)
+            side.wait_stream(cur)
+            ss = ctypes.c_void_p(side.cuda_stream)
+            _lib.check(lib.mrp_edge_encoder_bwd_prep(_ptr(dz), E, C, _ptr(dzT), E, ss), "mrp_edge_encoder_bwd_prep")
+            _lib.check(lib.mrp_edge_encoder_bwd_split(
+                None, _ptr(dzT), None, _ptr(hT), E, C, None, _ptr(dw2), _ptr(db2) if db2 is not None else None,
+                _ptr(wsa) if wsa is not None else None, nbytes, ss), "mrp_edge_encoder_bwd_split")
+            for t in (dz, hT, dzT, wsa, dw2, db2):
+                if t is not None:
+                    t.record_stream(side)
+        dw1 = db1 = dhT = None
+        if need[0] or need[1] or need[2]:  # dh^T = W2^T dz^T, then the ReLU mask, dW1, db1
+            w2t = w2t_get()
+            st = ctypes.c_void_p(cur.cuda_stream)
+            dhT = torch.empty((C, E), device=dev)
+            wsb = workspace()
+            _lib.check(lib.mrp_edge_encoder_bwd_split(
+                _ptr(dz), None, _ptr(w2t), None, E, C, _ptr(dhT), None, None,
+                _ptr(wsb) if wsb is not None else None, nbytes, st), "mrp_edge_encoder_bwd_split")
+            if need[1] or need[2]:
+                dw1 = out(1, (C, 9)) if need[1] else None
+                db1 = out(2, (C,)) if need[2] else None
+                wst = torch.empty(max(int(lib.mrp_edge_encoder_bwd_t_workspace(E, C)) // 4, 1), device=dev)
+                _lib.check(lib.mrp_edge_encoder_bwd_t(
+                    _ptr(dhT), E, _ptr(hT), E, _ptr(pose), E, C, _ptr(dw1) if dw1 is not None else None,
+                    _ptr(db1) if db1 is not None else None, _ptr(wst), wst.numel() * 4, st), "mrp_edge_encoder_bwd_t")
+        if side is not None:
+            cur.wait_stream(side)
+    dpose = pose_grad(dhT, hT, w1) if need[0] else None
+    return dpose, dw1, db1, dw2 if need[3] else None, db2
+
+
+def _pad32(n: int) -> int:
+    return (n + 31) // 32 * 32
+
+
+class _PaddedWeights:
+    """The encoder's weights zero-padded to C32 = C rounded up to 32 (W1 (C32, 9), b1 (C32), W2
+    (2 C32, C32) with W2 in its top-left (2C, C) corner, b2 (2 C32)) and their packed image: the
+    split kernels on these compute z's 2C columns exactly (every padded term a product with an exact
+    zero) in the first 2C columns of a (E, 2 C32) result."""
+
+    __slots__ = ("key", "C", "Cp", "w1", "b1", "w2", "b2", "img", "_w2t", "_w2t_img", "__weakref__")
+
+    def w2t(self):
+        if self._w2t is None:
+            self._w2t = self.w2.t().contiguous()
+        return self._w2t
+
+    def w2t_img(self):
+        if self._w2t_img is None:
+            self._w2t_img = _pack_w2t(self.w2)
+        return self._w2t_img
+
+
+_padded = weakref.WeakKeyDictionary()
+
+
+def padded_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> "_PaddedWeights":
+    """The zero-padded weights of an encoder whose C is not a multiple of 32 (or whose edge count is
+    not), rebuilt when a weight changes (the keys of :func:`packed_weights`)."""
+    w1, b1, w2, b2 = l1.weight, l1.bias, l2.weight, l2.bias
+    key = tuple((t.data_ptr(), t._version, t.device.index) for t in (w1, b1, w2) + ((b2,) if b2 is not None else ()))
+    hit = _padded.get(l2)
+    if hit is not None and hit.key == key:
+        return hit
+    C = w1.shape[0]
+    Cp = _pad32(C)
+    dev = w1.device
+    r = _PaddedWeights()
+    r.key, r.C, r.Cp, r._w2t, r._w2t_img = key, C, Cp, None, None
+    with torch.no_grad():
+        r.w1 = torch.zeros((Cp, 9), device=dev)
+        r.w1[:C] = w1
+        r.b1 = torch.zeros((Cp,), device=dev)
+        r.b1[:C] = b1
+        r.w2 = torch.zeros((2 * Cp, Cp), device=dev)
+        r.w2[: 2 * C, :C] = w2
+        r.b2 = torch.zeros((2 * Cp,), device=dev)
+        if b2 is not None:
+            r.b2[: 2 * C] = b2
+    r.img = _pack(r.w1, r.b1, r.w2)
+    _padded[l2] = r
+    return r
+
+
+def padded_supported(E: int, C: int) -> bool:
+    """The padded split path's shapes: the padded operands (E32 x 2 C32 floats at most) addressable
+    with 32-bit offsets and the padded weight image under 2^31 bytes."""
+    Ep, Cp = _pad32(E), _pad32(C)
+    return E > 0 and C > 0 and Ep * 2 * Cp * 4 < (1 << 31) and image_supported(Cp)
+
+
+class EdgeEncoderPaddedFunction(torch.autograd.Function):
+    """The split-bf16 training path (:class:`EdgeEncoderSplitFunction`'s kernels) for shapes it does not
+    tile: E and C rounded up to 32 with zero pose rows, zero weight rows/columns (``padded_weights``)
+    and zero gradient rows; z and every gradient are the leading blocks of the padded results."""
+
+    @staticmethod
+    def forward(ctx, pose, w1, b1, w2, b2, rec):
+        E, C, Cp = pose.shape[0], rec.C, rec.Cp
+        Ep = _pad32(E)
+        dev = pose.device
+        pp = torch.zeros((Ep, 9), device=dev)
+        pp[:E] = pose.detach()
+        zp = torch.empty((Ep, 2 * Cp), device=dev)
+        hT = torch.empty((Cp, Ep), device=dev)
+        lib = _lib.load_library()
+        with torch.cuda.device(dev):
+            _lib.check(lib.mrp_edge_encoder_fwd_split_train(
+                _ptr(pp), _ptr(rec.img), _ptr(rec.b2), Ep, Cp, _ptr(zp), _ptr(hT), Ep,
+                ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
+        ctx.save_for_backward(pp, hT)
+        ctx.rec, ctx.E = rec, E
+        ctx.has_b2 = b2 is not None
+        return zp[:E, : 2 * C].contiguous()
+
+    @staticmethod
+    def backward(ctx, dz):
+        pp, hT = ctx.saved_tensors
+        rec, E = ctx.rec, ctx.E
+        C, Cp = rec.C, rec.Cp
+        dev = dz.device
+        need = list(ctx.needs_input_grad[:5])
+        need[4] = need[4] and ctx.has_b2
+        dzp = torch.zeros((pp.shape[0], 2 * Cp), device=dev)
+        dzp[:E, : 2 * C] = dz
+        dpose, dw1, db1, dw2, db2 = split_backward(dzp, pp, hT, rec.w1, need,
+                                                   lambda i, shape: torch.empty(shape, device=dev),
+                                                   rec.w2t, rec.w2t_img)
+        return (dpose[:E] if dpose is not None else None,
+                dw1[:C].contiguous() if dw1 is not None else None,
+                db1[:C].contiguous() if db1 is not None else None,
+                dw2[: 2 * C, :C].contiguous() if dw2 is not None else None,
+                db2[: 2 * C].contiguous() if db2 is not None else None, None)
 
 
 def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Tensor:
@@ -407,11 +547,16 @@ def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Te
         if z is not None:
             PATH_COUNTS["split"] += 1
             return z
-    C = l1.weight.shape[0]
-    if _LOGITS_PATH == "split" and split_train_supported(pose.shape[0], C) and l1.bias is not None \
-            and tuple(l1.weight.shape) == (C, 9) and tuple(l2.weight.shape) == (2 * C, C):
-        PATH_COUNTS["split_train"] += 1
-        return EdgeEncoderSplitFunction.apply(pose, l1.weight, l1.bias, l2.weight, l2.bias,
-                                              packed_weights(l1, l2), l2)
+    C, E = l1.weight.shape[0], pose.shape[0]
+    if _LOGITS_PATH == "split" and l1.bias is not None and tuple(l1.weight.shape) == (C, 9) \
+            and tuple(l2.weight.shape) == (2 * C, C):
+        if split_train_supported(E, C):
+            PATH_COUNTS["split_train"] += 1
+            return EdgeEncoderSplitFunction.apply(pose, l1.weight, l1.bias, l2.weight, l2.bias,
+                                                  packed_weights(l1, l2), l2)
+        if padded_supported(E, C):
+            PATH_COUNTS["split_padded"] += 1
+            return EdgeEncoderPaddedFunction.apply(pose, l1.weight, l1.bias, l2.weight, l2.bias,
+                                                   padded_weights(l1, l2))
     PATH_COUNTS["autograd"] += 1
     return EdgeEncoderFunction.apply(*params)

@@ -97,7 +97,8 @@ def test_logits_kernel_vs_float64(cuda_device, E, C):
 
 
 def test_logits_kernel_declines_unsupported_shapes(cuda_device):
-    """C % 32 != 0: the ABI says NotSupported (and logits_forward takes the library GEMM instead)."""
+    """C % 32 != 0: the ABI says NotSupported (and logits_forward, on the comparison paths only, takes
+    the library GEMM instead; the product path pads, tests/test_gpu_encoder_train.py)."""
     h = torch.randn(10, 48, device=cuda_device)
     w2 = torch.randn(96, 48, device=cuda_device)
     b2 = torch.randn(96, device=cuda_device)
@@ -119,16 +120,18 @@ def _f64_logits(enc, pose):
 
 
 def test_edge_logits_takes_fused_kernel_only_without_grad(cuda_device):
-    """edge_logits: inference -> the one-launch split-bf16 kernel; with gradients wanted -> the
-    two-kernel autograd path; a shape the kernel declines (C % 32) -> the two-kernel path.  Both
-    within the float64 yardstick of the reference layers."""
+    """edge_logits: inference -> the one-launch split-bf16 kernel; with gradients wanted -> the split
+    training path (E % 32 == 0 and C % 32 == 0) or its zero-padded form (else); C = 48 runs both on
+    padded weights.  All within the float64 yardstick of the reference layers."""
     torch.manual_seed(0)
-    for C in (64, 48):
+    for C, E, path in ((64, 96, "split_train"), (64, 100, "split_padded"), (48, 100, "split_padded")):
         enc = m.edge_encoder([C, C]).to(cuda_device)
-        pose = torch.randn(100, 9, device=cuda_device)
+        pose = torch.randn(E, 9, device=cuda_device)
+        n_split, n_train = m.encoder.PATH_COUNTS["split"], m.encoder.PATH_COUNTS[path]
         with torch.no_grad():
             z0 = m.encoder.edge_logits(enc.layers, pose)
         z1 = m.encoder.edge_logits(enc.layers, pose)
+        assert m.encoder.PATH_COUNTS["split"] == n_split + 1 and m.encoder.PATH_COUNTS[path] == n_train + 1
         assert z1.requires_grad and not z0.requires_grad
         t32, z64 = _f64_logits(enc, pose)
         for z in (z0, z1.detach()):

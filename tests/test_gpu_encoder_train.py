@@ -39,14 +39,68 @@ def test_split_training_encoder_vs_float64(cuda_device, E, C, form):
         m.encoder.set_fused_backward(True)
 
 
-def _check_training_encoder(cuda_device, E, C, pose_grad):
+@pytest.mark.parametrize("form", ["fused", "two_stream", "pose_grad"])
+@pytest.mark.parametrize("E,C", [(1, 1), (7, 3), (100, 130), (33, 1281), (1000, 48), (56, 1000), (1792, 500),
+                                 (64, 96 + 1), (31, 32), (1793, 512)])
+def test_padded_training_encoder_vs_float64(cuda_device, E, C, form):
+    """E or C not a multiple of 32 (these trained on hipBLASLt GEMMs): the split-bf16
+    kernels on zero-padded operands (``EdgeEncoderPaddedFunction``), every form, every gradient
+    against float64 — e.g. ``feature_dim`` 1000 or 500, ragged edge counts, one channel."""
+    m.encoder.set_fused_backward(form != "two_stream")
+    try:
+        _check_training_encoder(cuda_device, E, C, pose_grad=form == "pose_grad", path="split_padded")
+    finally:
+        m.encoder.set_fused_backward(True)
+
+
+@pytest.mark.parametrize("E,C", [(1, 1), (100, 130), (33, 1281), (1000, 48), (1792, 500)])
+def test_padded_inference_encoder_vs_float64(cuda_device, E, C):
+    """No gradient wanted, C % 32 != 0: one ``mrp_edge_encoder_fwd_split`` launch on the padded weight
+    image, z its 2C leading columns; repacked after an in-place weight update."""
+    torch.manual_seed(E + 3 * C)
+    enc = m.edge_encoder([C, C]).to(cuda_device)
+    pose = (torch.randn(E, 9) * 8).to(cuda_device)
+    for step in range(2):
+        before = m.encoder.PATH_COUNTS["split"]
+        with torch.no_grad():
+            z = m.encoder.edge_logits(enc.layers, pose)
+        assert m.encoder.PATH_COUNTS["split"] == before + 1
+        assert z.shape == (E, 2 * C) and z.is_contiguous()
+        z32, _, _ = _reference(enc, pose, torch.zeros(E, 2 * C, device=cuda_device), torch.float32)
+        z64, _, _ = _reference(enc, pose, torch.zeros(E, 2 * C, device=cuda_device), torch.float64)
+        ok, errs = stack_ref.within(z, z32, z64)
+        assert ok, (step, errs)
+        with torch.no_grad():
+            for p in enc.parameters():
+                p.mul_(-1.25)  # an optimizer-like in-place update: the padded image is rebuilt
+
+
+@pytest.mark.parametrize("E,C", [(1, 32), (63, 64), (1792, 512), (100, 2048), (20000, 64), (4097, 1312)])
+def test_pose_gradient_kernel(cuda_device, E, C):
+    """``mrp_edge_encoder_bwd_pose`` (dpose = (dh^T (.) [h^T > 0])^T W1) against float64: one k slice
+    (many edges) and many (few edges, wide C), ragged 64-edge blocks."""
+    torch.manual_seed(E + C)
+    hT = torch.randn(C, E, device=cuda_device)
+    dhT = torch.randn(C, E, device=cuda_device)
+    w1 = torch.randn(C, 9, device=cuda_device)
+    got = m.encoder.pose_grad(dhT, hT, w1)
+    d = dhT * (hT > 0)
+    f32 = d.t().mm(w1)
+    f64 = d.double().t().mm(w1.double())
+    ok, errs = stack_ref.within(got, f32, f64)
+    assert ok, errs
+    again = m.encoder.pose_grad(dhT, hT, w1)
+    assert torch.equal(got, again)  # fixed summation order
+
+
+def _check_training_encoder(cuda_device, E, C, pose_grad, path="split_train"):
     torch.manual_seed(E + 7 * C)
     enc = m.edge_encoder([C, C]).to(cuda_device)
     pose = (torch.randn(E, 9) * 8).to(cuda_device).requires_grad_(pose_grad)
     gz = torch.randn(E, 2 * C, device=cuda_device)
-    before = m.encoder.PATH_COUNTS["split_train"]
+    before = m.encoder.PATH_COUNTS[path]
     z = m.encoder.edge_logits(enc.layers, pose)
-    assert m.encoder.PATH_COUNTS["split_train"] == before + 1
+    assert m.encoder.PATH_COUNTS[path] == before + 1
     z.backward(gz)
     z32, g32, p32 = _reference(enc, pose, gz, torch.float32)
     z64, g64, p64 = _reference(enc, pose, gz, torch.float64)
