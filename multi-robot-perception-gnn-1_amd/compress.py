@@ -22,10 +22,11 @@ built once per weight version (:func:`packed_weight`).
 The module keeps the reference's ``nn.Conv2d`` parameters (``conv1.weight`` (C, 2C, 1, 1),
 ``conv1.bias``), so ``state_dict`` keys are unchanged.
 
-Shapes the kernels decline (C % 32 != 0, H W % 4 != 0 — and, for the weight gradient only,
+Shapes the kernels do not tile (C % 32 != 0, H W % 4 != 0 — and, for the weight gradient only,
 H W % 32 != 0 — none of them a reference configuration: the reference's planes are
-``image_size/32`` squares, 8 x 8 at its default) run torch's own GEMMs
-(``set_compress_path("library")`` forces that path everywhere, for A/B measurements).
+``image_size/32`` squares, 8 x 8 at its default) run the same kernels on zero-padded operands
+(:func:`_fwd`, :func:`_bwd_data`, :func:`_bwd_weight`); ``set_compress_path("library")`` runs
+torch's own GEMMs everywhere, for A/B measurements only.
 """
 from __future__ import annotations
 
@@ -73,6 +74,7 @@ _packed = {}
 
 def clear_packed_weights() -> None:
     _packed.clear()
+    _padded_w.clear()
 
 
 def packed_weight(weight: torch.Tensor, kind: str) -> torch.Tensor:
@@ -269,8 +271,88 @@ def _lib_backward_weight(gy, x, a, want_bias):
     return torch.mm(g2, h2.t()).view(C, 2 * C, 1, 1), (gy.sum((0, 2, 3)) if want_bias else None)
 
 
-def _use_kernels(C, P) -> bool:
-    return _PATH[0] in ("hip", "split") and kernels_supported(C, P)
+# ---- shapes the kernels do not tile: the same kernels on zero-padded operands ---------------------
+# C rounded up to 32 and H W to 4 (forward, data gradient) or 32 (weight gradient): padded channels
+# carry zero features and zero weight rows / columns, padded pixels zero features and zero gradients,
+# so every padded term of every sum is a product with an exact zero and the results are the leading
+# blocks of the padded ones.
+
+def _round(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+# padded (weight, bias) per weight tensor, keyed like the packed images: id -> (weakref, key, wp, bp)
+_padded_w = {}
+
+
+def _padded_params(weight: torch.Tensor, bias):
+    key = (weight.data_ptr(), weight._version, weight.device.index) + \
+        ((bias.data_ptr(), bias._version) if bias is not None else ())
+    hit = _padded_w.get(id(weight))
+    if hit is not None and hit[0]() is weight and hit[1] == key:
+        return hit[2], hit[3]
+    C = weight.shape[0]
+    Cp = _round(C, 32)
+    w = _weight2d(weight)
+    with torch.no_grad():
+        wp = torch.zeros((Cp, 2 * Cp, 1, 1), device=w.device, dtype=torch.float32)
+        wp[:C, :C, 0, 0] = w[:, :C]
+        wp[:C, Cp:Cp + C, 0, 0] = w[:, C:]
+        bp = None
+        if bias is not None:
+            bp = torch.zeros((Cp,), device=w.device, dtype=torch.float32)
+            bp[:C] = bias.detach()
+    wid = id(weight)
+    _padded_w[wid] = (weakref.ref(weight, lambda _r, wid=wid: _padded_w.pop(wid, None)), key, wp, bp)
+    return wp, bp
+
+
+def _pad_planes(t: torch.Tensor, Cp: int, Pp: int) -> torch.Tensor:
+    """(N, C, H, W) -> (N, Cp, Pp, 1) with t in the leading (C, H W) block, zeros elsewhere."""
+    n, C, H, W = t.shape
+    out = torch.zeros((n, Cp, Pp, 1), device=t.device, dtype=torch.float32)
+    out.view(n, Cp, Pp)[:, :C, : H * W] = t.reshape(n, C, H * W)
+    return out
+
+
+def _unpad_planes(t: torch.Tensor, C: int, H: int, W: int) -> torch.Tensor:
+    n, Cp, Pp, _ = t.shape
+    return t.view(n, Cp, Pp)[:, :C, : H * W].contiguous().view(n, C, H, W)
+
+
+def _fwd(weight, bias, x, a):
+    n, C, H, W = x.shape
+    if kernels_supported(C, H * W):
+        return compress_forward(weight, bias, x, a)
+    Cp, Pp = _round(C, 32), _round(H * W, 4)
+    wp, bp = _padded_params(weight, bias)
+    y = compress_forward(wp, bp, _pad_planes(x, Cp, Pp), _pad_planes(a, Cp, Pp))
+    return _unpad_planes(y, C, H, W)
+
+
+def _bwd_data(weight, gy):
+    n, C, H, W = gy.shape
+    if kernels_supported(C, H * W):
+        return compress_backward_data(weight, gy)
+    Cp, Pp = _round(C, 32), _round(H * W, 4)
+    wp, _ = _padded_params(weight, None)
+    gx, ga = compress_backward_data(wp, _pad_planes(gy, Cp, Pp))
+    return _unpad_planes(gx, C, H, W), _unpad_planes(ga, C, H, W)
+
+
+def _bwd_weight(gy, x, a, want_bias, weight, bias, want_weight=True):
+    n, C, H, W = gy.shape
+    if kernels_supported(C, H * W):
+        r = compress_backward_weight(gy, x, a, want_bias, weight, bias, want_weight=want_weight)
+        if r is not None:
+            return r
+    Cp, Pp = _round(C, 32), _round(H * W, 32)
+    r = compress_backward_weight(*(_pad_planes(t, Cp, Pp) for t in (gy, x, a)), want_bias)
+    if r is None:
+        raise RuntimeError(f"mrp_gnn: the compress weight-gradient kernels declined the padded shape C={Cp}, HW={Pp}")
+    dwp, dbp = r
+    dw = torch.cat((dwp[:C, :C], dwp[:C, Cp:Cp + C]), 1)
+    return dw, (dbp[:C].contiguous() if dbp is not None else None)
 
 
 class CompressFunction(torch.autograd.Function):
@@ -278,9 +360,8 @@ class CompressFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, a, weight, bias):
-        n, C, H, W = x.shape
-        hip = _use_kernels(C, H * W)
-        y = compress_forward(weight, bias, x, a) if hip else _lib_forward(weight, bias, x, a)
+        hip = _PATH[0] != "library"
+        y = _fwd(weight, bias, x, a) if hip else _lib_forward(weight, bias, x, a)
         ctx.save_for_backward(x, a, weight)
         ctx.hip, ctx.has_bias = hip, bias is not None
         return y
@@ -290,10 +371,10 @@ class CompressFunction(torch.autograd.Function):
         x, a, weight = ctx.saved_tensors
         gx = ga = dw = db = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            gx, ga = compress_backward_data(weight, gy) if ctx.hip else _lib_backward_data(weight, gy)
+            gx, ga = _bwd_data(weight, gy) if ctx.hip else _lib_backward_data(weight, gy)
         if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
-            r = compress_backward_weight(gy, x, a, ctx.has_bias) if ctx.hip else None
-            dw, db = r if r is not None else _lib_backward_weight(gy, x, a, ctx.has_bias)
+            dw, db = _bwd_weight(gy, x, a, ctx.has_bias, None, None) if ctx.hip else \
+                _lib_backward_weight(gy, x, a, ctx.has_bias)
         return gx, ga, dw, db
 
 
@@ -357,8 +438,8 @@ class FilmCompressFunction(torch.autograd.Function):
         n, C, H, W = x.shape
         agg = torch.empty(x.shape, device=x.device, dtype=torch.float32)
         film_mean_forward_into(x, gb, csr, mode, agg)
-        hip = _use_kernels(C, H * W)
-        y = compress_forward(weight, bias, x, agg) if hip else _lib_forward(weight, bias, x, agg)
+        hip = _PATH[0] != "library"
+        y = _fwd(weight, bias, x, agg) if hip else _lib_forward(weight, bias, x, agg)
         ctx.save_for_backward(x, gb, agg, weight, bias)
         ctx.csr, ctx.mode, ctx.has_bias, ctx.hip = csr, mode, bias is not None, hip
         return y
@@ -370,15 +451,15 @@ class FilmCompressFunction(torch.autograd.Function):
         need_x, need_gb = ctx.needs_input_grad[0], gb is not None and ctx.needs_input_grad[1]
         dx = dgb = dw = db = None
         if need_x or need_gb:
-            gx, ga = compress_backward_data(weight, gy) if ctx.hip else _lib_backward_data(weight, gy)
+            gx, ga = _bwd_data(weight, gy) if ctx.hip else _lib_backward_data(weight, gy)
             dx, dgb = film_mean_backward(ga, x, gb, ctx.csr, ctx.mode, need_x, need_gb,
                                          grad_x_base=gx if need_x else None)
             if dgb is not None:
                 dgb = dgb.view(gb.shape).to(gb.dtype)
         if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
-            r = compress_backward_weight(gy, x, agg, ctx.has_bias and ctx.needs_input_grad[3], weight, bias,
-                                         want_weight=ctx.needs_input_grad[2]) if ctx.hip else None
-            dw, db = r if r is not None else _lib_backward_weight(gy, x, agg, ctx.has_bias)
+            dw, db = _bwd_weight(gy, x, agg, ctx.has_bias and ctx.needs_input_grad[3], weight, bias,
+                                 want_weight=ctx.needs_input_grad[2]) if ctx.hip else \
+                _lib_backward_weight(gy, x, agg, ctx.has_bias)
             if not ctx.needs_input_grad[2]:
                 dw = None
         return dx, dgb, dw, db, None, None

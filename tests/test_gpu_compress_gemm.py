@@ -81,10 +81,22 @@ def test_compress_gemm_matches_float64(cuda_device, n, C, H, W, path):
         _check(o, f32, f64, name)
 
 
-@pytest.mark.parametrize("n,C,H,W", [(6, 48, 8, 8), (4, 64, 3, 5), (5, 64, 4, 4)])
-def test_compress_function_declined_shapes(cuda_device, n, C, H, W):
-    """CompressFunction on shapes a kernel declines (C % 32, H W % 4, or H W % 32 for the weight
-    gradient) runs torch's GEMMs for that product and still matches float64."""
+def _no_library_gemm(monkeypatch):
+    """Make torch's GEMM forms of the compress (the A/B comparison path) fail if anything calls them."""
+    def boom(*_a, **_k):
+        raise AssertionError("a library GEMM ran on the product path")
+    for name in ("_lib_forward", "_lib_backward_data", "_lib_backward_weight"):
+        monkeypatch.setattr(m.compress, name, boom)
+
+
+@pytest.mark.parametrize("path", ["split", "hip"])
+@pytest.mark.parametrize("n,C,H,W", [(6, 48, 8, 8), (4, 64, 3, 5), (5, 64, 4, 4), (3, 100, 7, 7), (2, 1, 1, 1),
+                                     (4, 96, 6, 6), (2, 33, 9, 9)])
+def test_compress_function_declined_shapes(cuda_device, monkeypatch, n, C, H, W, path):
+    """CompressFunction on shapes the kernels do not tile (C % 32, H W % 4, or H W % 32 for the weight
+    gradient): the same kernels on zero-padded operands — never torch's GEMMs — and
+    every output and gradient against float64."""
+    _no_library_gemm(monkeypatch)
     torch.manual_seed(n + C + H)
     dev = cuda_device
     w = (torch.randn(C, 2 * C, 1, 1, device=dev) / (2 * C) ** 0.5).requires_grad_(True)
@@ -92,12 +104,19 @@ def test_compress_function_declined_shapes(cuda_device, n, C, H, W):
     x = torch.randn(n, C, H, W, device=dev, requires_grad=True)
     a = torch.randn(n, C, H, W, device=dev, requires_grad=True)
     gy = torch.randn(n, C, H, W, device=dev)
-    y = m.compress.CompressFunction.apply(x, a, w, b)
-    y.backward(gy)
-    r64 = _ref(w.detach(), b.detach(), x.detach(), a.detach(), gy, torch.float64)
-    r32 = _ref(w.detach(), b.detach(), x.detach(), a.detach(), gy, torch.float32)
-    for name, o, f32, f64 in zip(("y", "gx", "ga", "gw", "gb"), (y, x.grad, a.grad, w.grad, b.grad), r32, r64):
-        _check(o, f32, f64, name)
+    with _path(path):
+        for step in range(2):  # the second after an in-place weight update: padded weights rebuilt
+            for t in (w, b, x, a):
+                t.grad = None
+            y = m.compress.CompressFunction.apply(x, a, w, b)
+            y.backward(gy)
+            r64 = _ref(w.detach(), b.detach(), x.detach(), a.detach(), gy, torch.float64)
+            r32 = _ref(w.detach(), b.detach(), x.detach(), a.detach(), gy, torch.float32)
+            for name, o, f32, f64 in zip(("y", "gx", "ga", "gw", "gb"), (y, x.grad, a.grad, w.grad, b.grad), r32, r64):
+                _check(o, f32, f64, f"{name} (step {step})")
+            with torch.no_grad():
+                w.mul_(-0.5)
+                b.add_(1.0)
 
 
 @pytest.mark.parametrize("path", PATHS)

@@ -86,6 +86,22 @@ def test_config4_full_size(cuda_device):
     check_config(cuda_device, B=8, N=16, C=1024, H=16, layers=3, knn=4)
 
 
+@pytest.mark.parametrize("B,N,C,H,layers,knn", [(3, 5, 48, 7, 2, None), (2, 8, 100, 6, 1, None),
+                                                 (2, 10, 40, 5, 2, 3)])
+def test_odd_shapes_stay_on_hip_kernels(cuda_device, monkeypatch, B, N, C, H, layers, knn):
+    """A user of the reference with ``feature_dim`` and plane sizes no BASELINE config has (C % 32 != 0,
+    H W % 4 != 0): the encoder and the compress run the hand-written kernels on zero-padded operands
+    (no library GEMM: the comparison forms are patched to fail), forward and every gradient against
+    float64."""
+    def boom(*_a, **_k):
+        raise AssertionError("a library GEMM ran on the product path")
+    for name in ("_lib_forward", "_lib_backward_data", "_lib_backward_weight"):
+        monkeypatch.setattr(m.compress, name, boom)
+    before = m.encoder.PATH_COUNTS["autograd"]
+    check_config(cuda_device, B=B, N=N, C=C, H=H, layers=layers, knn=knn)
+    assert m.encoder.PATH_COUNTS["autograd"] == before  # the fp32 encoder (library backward) never ran
+
+
 def test_config1_full_size(cuda_device):
     """configs[1]: 8-robot warehouse, ResNet18 C=512 at H/8 x W/8 = 32x32, batch 16, 2 layers (multi_gcn +
     compress, ``dgl/model/models.py:180-189``) — the grid sizes the benchmark runs (forward, dx and
