@@ -316,27 +316,19 @@ int mrp_edge_logits_fwd(const float* h, int32_t num_edges, int32_t C, const floa
  *                                   and b2 (2C, or NULL) -> z (E, 2C)
  * Requirements (else hipErrorNotSupported): C % 32 == 0 and a packed image below 2^31 bytes (the
  * kernel addresses it with 32-bit offsets: C <= 13344).  The z accumulation keeps the a0 b0 products
- * apart from the five small ones (two accumulators per output, summed once).
- * workspace: NULL/0, or >= mrp_edge_encoder_fwd_split_workspace(E, C) bytes (16-byte aligned, zeroed
- * before its first use, then reusable by later calls of the same (E, C) on the same stream — a call
- * leaves the words it counts with at zero, but another shape's counters sit where this one's partial
- * sums go — and never by two streams at once): with it the hidden blocks may run in slices (split-K over workgroups, "edge_ks"), the last
- * workgroup of each tile summing the slices' partials in slice order (deterministic) and restoring
- * the workspace's counters to zero; without it (or 0 bytes asked) one pass.  The result depends on
- * the slice count (fp32 rounding), never on timing.
+ * apart from the five small ones (two accumulators per output, summed once).  Used for inference;
+ * training keeps h for its backward and runs mrp_edge_hidden_fwd + mrp_edge_logits_fwd.
  */
 int64_t mrp_edge_encoder_pack_bytes(int32_t C);
 int mrp_edge_encoder_pack(const float* w1, const float* b1, const float* w2, int32_t C, void* packed, void* stream);
-int64_t mrp_edge_encoder_fwd_split_workspace(int32_t num_edges, int32_t C);
 int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const float* b2, int32_t num_edges, int32_t C,
-                               float* z, void* workspace, int64_t workspace_bytes, void* stream);
+                               float* z, void* stream);
 
 /*
  * The encoder's training path on the split-bf16 matrix cores (replaces mrp_edge_hidden_fwd +
  * mrp_edge_logits_fwd forward and the two library GEMMs of the backward, dgl/model/models.py:146-149
  * under dgl/training.py:208-210's loss.backward()):
- *   mrp_edge_encoder_fwd_split_train   as mrp_edge_encoder_fwd_split (shared-hidden form, the same
- *                                      workspace contract and the same z bits), and also
+ *   mrp_edge_encoder_fwd_split_train   as mrp_edge_encoder_fwd_split (shared-hidden form), and also
  *                                      h^T = relu(pose W1^T + b1)^T, (C, E) rows of hT_stride >= E floats
  *   mrp_edge_encoder_bwd_prep          dzT (2C, E) rows of dzT_stride >= E = dz^T (E % 4 == 0, C even,
  *                                      16-byte aligned, dzT_stride % 4 == 0; else hipErrorNotSupported)
@@ -370,8 +362,7 @@ int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const floa
  * deterministic.
  */
 int mrp_edge_encoder_fwd_split_train(const float* pose, const void* packed, const float* b2, int32_t num_edges,
-                                     int32_t C, float* z, float* hT, int64_t hT_stride, void* workspace,
-                                     int64_t workspace_bytes, void* stream);
+                                     int32_t C, float* z, float* hT, int64_t hT_stride, void* stream);
 int mrp_edge_encoder_bwd_prep(const float* dz, int32_t num_edges, int32_t C, float* dzT, int64_t dzT_stride,
                               void* stream);
 int64_t mrp_edge_encoder_bwd_split_workspace(int32_t num_edges, int32_t C);
@@ -448,14 +439,12 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
  * forward / data gradient, "nt_group" (the same, default 0) for the weight gradient; "enc_bwd_psa"
  * (mrp_edge_encoder_bwd_fused given w2T_packed: 2 default = both products read their A operand
  * pre-split, dz^T written as a packed image; 1 = only W2^T's image; 0 = both split in the kernel);
- * "enc_s1" / "enc_s2" (its two products' split-K counts, 0 = the planner's); "edge_ks" (hidden-block slices of
- * mrp_edge_encoder_fwd_split(_train) given a workspace: 0 per shape, 1, 2 or 4). */
+ * "enc_s1" / "enc_s2" (its two products' split-K counts, 0 = the planner's). */
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 21 = this header: v19 plus
- * the streaming yardstick mrp_stream_copy, the encoder's pose gradient (mrp_edge_encoder_bwd_pose
- * + workspace) and a split-K workspace on the encoder's forward entry points
- * (mrp_edge_encoder_fwd_split_workspace); 20: v19 plus a one-launch no-grad GCN layer
+ * the streaming yardstick mrp_stream_copy and the encoder's pose gradient (mrp_edge_encoder_bwd_pose
+ * + workspace); 20: v19 plus a one-launch no-grad GCN layer
  * (mrp_gcn_fwd_fused), measured slower than the two launches it replaced and removed in 21
  * (tools/lab_patches/r06_fused_layer.patch); 19: v18 with
  * mrp_edge_encoder_bwd_fused taking W2^T's packed image (w2T_packed); 18: v17 without

@@ -40,7 +40,6 @@ EXPORTED_SYMBOLS = (
     "mrp_edge_logits_fwd",
     "mrp_edge_encoder_pack_bytes",
     "mrp_edge_encoder_pack",
-    "mrp_edge_encoder_fwd_split_workspace",
     "mrp_edge_encoder_fwd_split",
     "mrp_edge_encoder_fwd_split_train",
     "mrp_edge_encoder_bwd_workspace",
@@ -145,11 +144,9 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_edge_encoder_pack_bytes.restype = ctypes.c_int64
     lib.mrp_edge_encoder_pack.argtypes = [_P, _P, _P, _I32, _P, _P]
     lib.mrp_edge_encoder_pack.restype = ctypes.c_int
-    lib.mrp_edge_encoder_fwd_split_workspace.argtypes = [_I32, _I32]
-    lib.mrp_edge_encoder_fwd_split_workspace.restype = ctypes.c_int64
-    lib.mrp_edge_encoder_fwd_split.argtypes = [_P, _P, _P, _I32, _I32, _P, _P, _I64, _P]
+    lib.mrp_edge_encoder_fwd_split.argtypes = [_P, _P, _P, _I32, _I32, _P, _P]
     lib.mrp_edge_encoder_fwd_split.restype = ctypes.c_int
-    lib.mrp_edge_encoder_fwd_split_train.argtypes = [_P, _P, _P, _I32, _I32, _P, _P, _I64, _P, _I64, _P]
+    lib.mrp_edge_encoder_fwd_split_train.argtypes = [_P, _P, _P, _I32, _I32, _P, _P, _I64, _P]
     lib.mrp_edge_encoder_fwd_split_train.restype = ctypes.c_int
     lib.mrp_edge_encoder_bwd_prep.argtypes = [_P, _I32, _I32, _P, _I64, _P]
     lib.mrp_edge_encoder_bwd_prep.restype = ctypes.c_int

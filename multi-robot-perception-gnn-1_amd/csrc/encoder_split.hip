@@ -14,25 +14,15 @@
 // it against float64 with the same yardstick as the fp32 kernels); it runs on
 // v_mfma_f32_32x32x16_bf16, six of which cost 192 cycles per 16 k against 512 for the fp32 MFMA.
 //
-// Structure.  One wave owns 32 edges x 64 output columns; the four waves of a workgroup share a
-// column slab, whose weight fragments arrive once per workgroup by LDS-DMA (four stages, two ahead).
-// Per block of 32 hidden units a wave
-//   1. computes X = W1' pose'^T (32 units x 32 edges) on the MFMAs: k = the 9 pose values, then 1.0
-//      against b1 (so the bias is one more product), zero-padded to 16;
-//   2. applies the ReLU and splits X into bf16 parts in registers — X's accumulator layout (edge on
-//      the lane, units in the registers) IS the A operand of z = X^T W2^T (a sum over X's row index:
-//      cdna_hip_programming.md §3, accumulator as operand) with a permuted k order inside each 16-k
-//      step, which the packed W2 image reproduces;
-//   3. accumulates z for its 64 columns (two 32 x 32 blocks).
-// The weights are split and laid out once per weight version by mrp_edge_encoder_pack, in the exact
-// per-lane fragment order, so every weight load of a wave is one contiguous KiB.
-// Hidden split (KS = 2, C % 64 == 0): the workgroup's eight waves are two sets of four, each set
-// walking half of the hidden blocks with its own LDS stage ring; the second set's z partials are
-// added to the first's through LDS at the end (a fixed order: deterministic).  Two waves per SIMD
-// then overlap one wave's ReLU/split (VALU) and LDS reads with the other's MFMAs, where one wave per
-// SIMD serialised them, and each wave's dependent chain is half as long.
-// Work per launch at the headline (E = 1792, C = 512): 224 workgroups of 4 KS waves; h is computed
-// once per (32 edges, 64 columns, hidden block): 6 MFMAs per hidden block against 24 for z.
+// Structure: the shared-hidden form below (encoder2_body).  A workgroup of 4 or 8 waves owns one
+// block of 32 edges and one 32-column block of z per wave; the hidden layer X (32 units x 32 edges per
+// hidden block) is computed on the MFMAs by the waves in turn, ReLU'd, split and shared through LDS
+// slots, and every wave runs z for its own columns with its W2 fragments loaded from the packed image
+// straight into registers, four sets in rotation.  Round 3's per-wave form and the two-column-block
+// and hidden-split forms are lab code (tools/lab_encoder_r3.hip); round 6's split-K over workgroups
+// (hidden-block slices, the last arriver of a tile summing the partials) measured slower at the
+// headline — 23.4 / 26.0 us for 2 / 4 slices against 21.8 in-step — and is kept as
+// tools/lab_patches/r06_encoder_splitk.patch.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -88,12 +78,6 @@ struct FwdArgs {
   float* hT;     // shared-hidden forms, training: relu(pose W1^T + b1) transposed, (C, E) rows of hts floats
   int64_t hts;
   int32_t E, C, egroups;
-  // split-K (ks > 1): the hidden blocks in ks slices, one workgroup per (edge block, column group,
-  // slice); each writes its slice's partial z to part[slice] (ks x E x 2C floats), the last of a tile's
-  // ks workgroups to arrive (cnt[tile], restored to 0 by it) sums them in slice order into z
-  int32_t ks;
-  float* part;
-  uint32_t* cnt;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -121,11 +105,8 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-  // split-K: a tile's ks slices are consecutive ids (one XCD: the partials stay in its L2)
-  const int kss = id % a.ks, tid2 = id / a.ks;
-  const int eb = tid2 % eblocks, cg = tid2 / eblocks;
+  const int eb = id % eblocks, cg = id / eblocks;
   const int ngroups = (ncb + CPG - 1) / CPG;
-  const int HBk = HB / a.ks, hb0 = kss * HBk;  // this workgroup's hidden blocks [hb0, hb0 + HBk)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hh = lane >> 5;
@@ -194,7 +175,7 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
     // each register's 32 lanes store 128 contiguous bytes of a row)
     if constexpr (ALLX) {
       Xk[buf] = X;
-    } else if (a.hT != nullptr && hbx % ngroups == cg && hbx < hb0 + HBk && e0 + r < a.E) {
+    } else if (a.hT != nullptr && hbx % ngroups == cg && hbx < HB && e0 + r < a.E) {
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         a.hT[(int64_t)(hbx * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh) * a.hts + e0 + r] = relu(X[i]);
@@ -243,42 +224,42 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
       }
   };
 
-  const int rounds = (HBk + NWV - 1) / NWV;
-  // W2 fragments of hidden blocks t in set t % 4, requested three blocks ahead (one block's z is 12 CB
+  const int rounds = (HB + NWV - 1) / NWV;
+  // W2 fragments of hidden blocks hb in set hb % 4, requested three blocks ahead (one block's z is 12 CB
   // MFMAs per wave: too short to cover an L2 round trip under load); NWV % 4 == 0, so a round's
-  // blocks take the sets in a fixed order.  t counts this workgroup's blocks, hb0 + t is the block.
+  // blocks take the sets in a fixed order
   static_assert(NWV % 4 == 0, "four W2 sets per round");
   W2F f0, f1, f2, f3;
-  // every hidden block fits the two slot sets (HBk <= 2 NWV: C <= 512 with 8 waves): all of X first — each
-  // wave computes blocks w and w + NWV — one barrier, then z straight through all HBk blocks with no
+  // every hidden block fits the two slot sets (HB <= 2 NWV: C <= 512 with 8 waves): all of X first — each
+  // wave computes blocks w and w + NWV — one barrier, then z straight through all HB blocks with no
   // further barrier or X in between (the rounds below put a barrier and a VALU split phase between
   // every NWV blocks, with both waves of a SIMD in the split at the same time)
-  constexpr bool allx = ALLX;  // the launcher's choice: HBk <= 2 NWV
-  load_w1(hb0 + w);
-  if (allx && w + NWV < HBk) load_w1_into(hb0 + w + NWV, w1g);
-  load_w2(hb0, f0);
-  if (1 < HBk) load_w2(hb0 + 1, f1);
-  if (2 < HBk) load_w2(hb0 + 2, f2);
-  x_store(0, w < HBk ? hb0 + w : HB);
+  constexpr bool allx = ALLX;  // the launcher's choice: HB <= 2 NWV
+  load_w1(w);
+  if (allx && w + NWV < HB) load_w1_into(w + NWV, w1g);
+  load_w2(0, f0);
+  if (1 < HB) load_w2(1, f1);
+  if (2 < HB) load_w2(2, f2);
+  x_store(0, w);
   if constexpr (allx) {
-    if (w + NWV < HBk) x_store_from(1, hb0 + w + NWV, w1g);
+    if (w + NWV < HB) x_store_from(1, w + NWV, w1g);
     __syncthreads();
 #pragma unroll 1
-    for (int t = 0; t < HBk; t += 4) {
-      if (t + 3 < HBk) load_w2(hb0 + t + 3, f3);
-      z_block(t / NWV, t % NWV, f0);
-      if (t + 4 < HBk) load_w2(hb0 + t + 4, f0);
-      if (t + 1 < HBk) z_block((t + 1) / NWV, (t + 1) % NWV, f1);
-      if (t + 5 < HBk) load_w2(hb0 + t + 5, f1);
-      if (t + 2 < HBk) z_block((t + 2) / NWV, (t + 2) % NWV, f2);
-      if (t + 6 < HBk) load_w2(hb0 + t + 6, f2);
-      if (t + 3 < HBk) z_block((t + 3) / NWV, (t + 3) % NWV, f3);
+    for (int hb = 0; hb < HB; hb += 4) {
+      if (hb + 3 < HB) load_w2(hb + 3, f3);
+      z_block(hb / NWV, hb % NWV, f0);
+      if (hb + 4 < HB) load_w2(hb + 4, f0);
+      if (hb + 1 < HB) z_block((hb + 1) / NWV, (hb + 1) % NWV, f1);
+      if (hb + 5 < HB) load_w2(hb + 5, f1);
+      if (hb + 2 < HB) z_block((hb + 2) / NWV, (hb + 2) % NWV, f2);
+      if (hb + 6 < HB) load_w2(hb + 6, f2);
+      if (hb + 3 < HB) z_block((hb + 3) / NWV, (hb + 3) % NWV, f3);
     }
     if (a.hT != nullptr && e0 + r < a.E) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int tx = w + q * NWV, hbx = hb0 + tx;
-        if (tx < HBk && hbx % ngroups == cg) {
+        const int hbx = w + q * NWV;
+        if (hbx < HB && hbx % ngroups == cg) {
 #pragma unroll
           for (int i = 0; i < 16; ++i)
             a.hT[(int64_t)(hbx * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh) * a.hts + e0 + r] = relu(Xk[q][i]);
@@ -291,79 +272,25 @@ __device__ __forceinline__ void encoder2_body(const FwdArgs& a) {
   for (int rd = 0; rd < rounds; ++rd) {
     const int buf = rd & 1;
     const bool more = rd + 1 < rounds;
-    if (more) load_w1(hb0 + (rd + 1) * NWV + w);  // the next round's X, under this round's MFMAs
+    if (more) load_w1((rd + 1) * NWV + w);  // the next round's X, under this round's MFMAs
 #pragma unroll
     for (int j = 0; j < NWV; j += 4) {
-      const int t = rd * NWV + j;
-      if (t + 3 < HBk) load_w2(hb0 + t + 3, f3);
-      if (t < HBk) z_block(buf, j, f0);
-      if (t + 4 < HBk) load_w2(hb0 + t + 4, f0);
-      if (t + 1 < HBk) z_block(buf, j + 1, f1);
-      if (t + 5 < HBk) load_w2(hb0 + t + 5, f1);
-      if (t + 2 < HBk) z_block(buf, j + 2, f2);
-      if (t + 6 < HBk) load_w2(hb0 + t + 6, f2);
-      if (t + 3 < HBk) z_block(buf, j + 3, f3);
+      const int hb = rd * NWV + j;
+      if (hb + 3 < HB) load_w2(hb + 3, f3);
+      if (hb < HB) z_block(buf, j, f0);
+      if (hb + 4 < HB) load_w2(hb + 4, f0);
+      if (hb + 1 < HB) z_block(buf, j + 1, f1);
+      if (hb + 5 < HB) load_w2(hb + 5, f1);
+      if (hb + 2 < HB) z_block(buf, j + 2, f2);
+      if (hb + 6 < HB) load_w2(hb + 6, f2);
+      if (hb + 3 < HB) z_block(buf, j + 3, f3);
     }
-    if (more) {  // slot buf ^ 1: last read in round rd - 1, before the last barrier
-      const int tx = (rd + 1) * NWV + w;
-      x_store(buf ^ 1, tx < HBk ? hb0 + tx : HB);
-    }
+    if (more) x_store(buf ^ 1, (rd + 1) * NWV + w);  // slot buf ^ 1: last read in round rd - 1, before the last barrier
     if (!(ABL & 4)) __syncthreads();
   }
   }
   // epilogue: accumulator register i of lane (r, hh) is edge e0 + (i & 3) + 8 (i >> 2) + 4 hh, column r
   const int N = 2 * a.C;
-  if (a.ks > 1) {
-    // split-K: publish this slice's partial (write-through stores, drained by every wave before the
-    // barrier), count the tile's arrivals (agent scope); the last arriver reads the other slices'
-    // partials past its L1 and sums all ks in slice order — the same sum whichever arrives last
-    __shared__ uint32_t last;
-    float* mine = a.part + (int64_t)kss * a.E * N;
-#pragma unroll
-    for (int c = 0; c < CB; ++c) {
-      if (cbw[c] >= ncb) continue;
-      const int col = cbw[c] * 32 + r;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int e = e0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        if (e < a.E)
-          __hip_atomic_store(reinterpret_cast<uint32_t*>(mine + (int64_t)e * N + col),
-                             __float_as_uint(__fadd_rn(Z[c][i], ZL[c][i])), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int tile = tid2;
-    if (threadIdx.x == 0) {
-      const uint32_t seen = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = seen == (uint32_t)(a.ks - 1);
-      if (last) __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!last) return;
-#pragma unroll
-    for (int c = 0; c < CB; ++c) {
-      if (cbw[c] >= ncb) continue;
-      const int col = cbw[c] * 32 + r;
-      const float bias = a.b2 != nullptr ? a.b2[col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int e = e0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        if (e >= a.E) continue;
-        const int64_t off = (int64_t)e * N + col;
-        float v = 0.f;
-        for (int k = 0; k < a.ks; ++k) {
-          const float pk = k == kss ? __fadd_rn(Z[c][i], ZL[c][i])
-                                    : __uint_as_float(__hip_atomic_load(
-                                          reinterpret_cast<const uint32_t*>(a.part + (int64_t)k * a.E * N + off),
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          v = k == 0 ? pk : __fadd_rn(v, pk);
-        }
-        a.z[off] = __fadd_rn(v, bias);
-      }
-    }
-    return;
-  }
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
     if (cbw[c] >= ncb) continue;
@@ -387,7 +314,7 @@ template <int CB, int NWV>
 hipError_t launch2_cfg(void (*kern)(FwdArgs), const FwdArgs& a, hipStream_t st) {
   const int64_t eblocks = (a.E + 31) / 32;
   const int64_t groups = (2 * (int64_t)a.C / 32 + NWV * CB - 1) / (NWV * CB);
-  const int64_t grid = eblocks * groups * a.ks;
+  const int64_t grid = eblocks * groups;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   const size_t lds = (size_t)2 * NWV * 6 * 64 * 16;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NWV), lds, st, a);
@@ -395,7 +322,7 @@ hipError_t launch2_cfg(void (*kern)(FwdArgs), const FwdArgs& a, hipStream_t st) 
 }
 
 hipError_t launch_fwd2(int nwv, const FwdArgs& a, hipStream_t st) {
-  const bool allx = a.C / 32 / a.ks <= 2 * nwv && mrp_host::tuning().edge_allx;  // every X before z (encoder2_body)
+  const bool allx = a.C / 32 <= 2 * nwv && mrp_host::tuning().edge_allx;  // every X before z (encoder2_body)
   if (nwv == 8)
     return allx ? launch2_cfg<1, 8>(encoder2_cb1_w8_allx, a, st) : launch2_cfg<1, 8>(encoder2_cb1_w8, a, st);
   return allx ? launch2_cfg<1, 4>(encoder2_cb1_w4_allx, a, st) : launch2_cfg<1, 4>(encoder2_cb1_w4, a, st);
@@ -417,25 +344,6 @@ int fwd2_waves(int32_t num_edges, int32_t C) {
     v = grid8 >= 192 && grid8 <= 256 ? 3 : 1;
   }
   return v == 3 ? 8 : 4;
-}
-
-// hidden-block slices (split-K) per shape: mrp_tuning_set "edge_ks" (1, 2 or 4; 0 = the per-shape
-// choice below), only where the slices divide the hidden blocks
-int fwd2_slices(int32_t num_edges, int32_t C) {
-  int ks = mrp_host::tuning().edge_ks;
-  if (ks <= 0) ks = 1;
-  const int HB = C / 32;
-  while (ks > 1 && HB % ks != 0) ks >>= 1;
-  (void)num_edges;
-  return ks;
-}
-
-// split-K workspace: ks x E x 2C partial floats, then one arrival counter per tile (zero between
-// launches: the last arriver of each tile restores it)
-int64_t slices_bytes(int32_t E, int32_t C, int ks, int nwv) {
-  if (ks <= 1) return 0;
-  const int64_t tiles = ((int64_t)(E + 31) / 32) * ((2 * (int64_t)C / 32 + nwv - 1) / nwv);
-  return ((int64_t)ks * E * 2 * C * 4 + 255) / 256 * 256 + tiles * 4;
 }
 
 }  // namespace mrp_x6
@@ -465,30 +373,8 @@ extern "C" int mrp_edge_encoder_pack(const float* w1, const float* b1, const flo
   return hipGetLastError();
 }
 
-namespace {
-// the split-K slices of this call: 1 unless the workspace holds the slices' partials and counters
-int call_slices(int32_t E, int32_t C, void* workspace, int64_t workspace_bytes, FwdArgs& a) {
-  const int nwv = fwd2_waves(E, C);
-  int ks = fwd2_slices(E, C);
-  if (ks > 1 && (workspace == nullptr || (reinterpret_cast<uintptr_t>(workspace) & 15) ||
-                 workspace_bytes < slices_bytes(E, C, ks, nwv) || (int64_t)ks * E * 2 * C >= ((int64_t)1 << 31)))
-    ks = 1;
-  a.ks = ks;
-  a.part = static_cast<float*>(workspace);
-  a.cnt = ks > 1 ? reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) +
-                                                ((int64_t)ks * E * 2 * C * 4 + 255) / 256 * 256)
-                 : nullptr;
-  return nwv;
-}
-}  // namespace
-
-extern "C" int64_t mrp_edge_encoder_fwd_split_workspace(int32_t num_edges, int32_t C) {
-  if (num_edges <= 0 || C <= 0 || C % 32 != 0) return 0;
-  return slices_bytes(num_edges, C, fwd2_slices(num_edges, C), fwd2_waves(num_edges, C));
-}
-
 extern "C" int mrp_edge_encoder_fwd_split(const float* pose, const void* packed, const float* b2, int32_t num_edges,
-                                          int32_t C, float* z, void* workspace, int64_t workspace_bytes, void* stream) {
+                                          int32_t C, float* z, void* stream) {
   if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
   if (num_edges == 0 || C == 0) return hipSuccess;
   if (C % 32 != 0 || !image_fits(C)) return hipErrorNotSupported;
@@ -503,13 +389,12 @@ extern "C" int mrp_edge_encoder_fwd_split(const float* pose, const void* packed,
   a.E = num_edges;
   a.C = C;
   a.egroups = (num_edges + 127) / 128;
-  const int nwv = call_slices(num_edges, C, workspace, workspace_bytes, a);
-  return launch_fwd2(nwv, a, static_cast<hipStream_t>(stream));
+  return launch_fwd2(fwd2_waves(num_edges, C), a, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int mrp_edge_encoder_fwd_split_train(const float* pose, const void* packed, const float* b2,
                                                 int32_t num_edges, int32_t C, float* z, float* hT, int64_t hT_stride,
-                                                void* workspace, int64_t workspace_bytes, void* stream) {
+                                                void* stream) {
   if (num_edges < 0 || C < 0) return hipErrorInvalidValue;
   if (num_edges == 0 || C == 0) return hipSuccess;
   if (C % 32 != 0 || !image_fits(C)) return hipErrorNotSupported;
@@ -526,6 +411,5 @@ extern "C" int mrp_edge_encoder_fwd_split_train(const float* pose, const void* p
   a.C = C;
   a.egroups = (num_edges + 127) / 128;
   // the shared-hidden form, its column groups sharing the h^T stores (per-shape choice as the inference entry)
-  const int nwv = call_slices(num_edges, C, workspace, workspace_bytes, a);
-  return launch_fwd2(nwv, a, static_cast<hipStream_t>(stream));
+  return launch_fwd2(fwd2_waves(num_edges, C), a, static_cast<hipStream_t>(stream));
 }

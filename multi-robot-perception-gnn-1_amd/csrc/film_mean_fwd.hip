@@ -114,7 +114,6 @@ int mrp_tuning_set(const char* name, int32_t value) {
       {"bwd_mfma_cpw", &t.bwd_mfma_cpw, 1, 2},
       {"edge_split_v", &t.edge_split_v, -1, 3},
       {"edge_allx", &t.edge_allx, 0, 1},
-      {"edge_ks", &t.edge_ks, 0, 4},
       {"gemm_split", &t.gemm_split, -1, 7},
       {"split_nt", &t.split_nt, -1, 4},
       {"gemm_group", &t.gemm_group, 0, 64},
@@ -131,7 +130,6 @@ int mrp_tuning_set(const char* name, int32_t value) {
       if (k.field == &t.gemm_split && value != -1 && value != 2 && value != 7) return hipErrorInvalidValue;
       if (k.field == &t.split_nt && value != -1 && value != 3 && value != 4) return hipErrorInvalidValue;
       if (k.field == &t.edge_split_v && value != -1 && value != 1 && value != 3) return hipErrorInvalidValue;
-      if (k.field == &t.edge_ks && value == 3) return hipErrorInvalidValue;
       *k.field = value;
       return hipSuccess;
     }

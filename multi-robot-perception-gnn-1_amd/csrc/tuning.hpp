@@ -38,9 +38,6 @@ struct Tuning {
   // mrp_edge_encoder_fwd_split (encoder_split.hip): -1 per shape, 1 = 4 waves, 3 = 8 waves per workgroup
   int edge_split_v = -1;
   int edge_allx = 1;  // mrp_edge_encoder_fwd_split: all hidden blocks before z where they fit LDS (0 off)
-  // mrp_edge_encoder_fwd_split(_train): hidden-block slices (split-K across workgroups, the last arriver
-  // of a tile summing the partials in slice order) — 0 = per shape, 1 / 2 / 4
-  int edge_ks = 0;
   // split-bf16 weight-gradient (NT) kernel: 4 (the default where C >= 1024) the compress weight gradient
   // with dy split once into a packed image (split_rows + gemm_nt_psa) where the image fits 32-bit
   // offsets, else (and for the encoder's products) 3 (the default below C = 1024): the 32-k-stage form

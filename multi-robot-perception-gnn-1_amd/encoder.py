@@ -107,32 +107,6 @@ def packed_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> torch.Tensor:
     return img
 
 
-# split-K workspaces of the forward kernels, per (device, stream, shape): zeroed when allocated — the
-# kernels leave their arrival counters at zero after every launch, but the counters of one shape sit
-# where another shape's partial sums go, so a workspace serves one shape — and never shared by two
-# streams.  The few most recent shapes per device and stream are kept.
-_fwd_ws = collections.OrderedDict()
-_FWD_WS_KEEP = 8
-
-
-def fwd_workspace(dev: torch.device, E: int, C: int):
-    """(workspace tensor or None, bytes) for ``mrp_edge_encoder_fwd_split(_train)`` at (E, C) on the
-    current stream of ``dev``."""
-    nbytes = int(_lib.load_library().mrp_edge_encoder_fwd_split_workspace(E, C))
-    if nbytes <= 0:
-        return None, 0
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, E, C, nbytes)
-    ws = _fwd_ws.get(key)
-    if ws is None:
-        ws = torch.zeros((nbytes + 3) // 4, device=dev, dtype=torch.int32)
-        _fwd_ws[key] = ws
-        while len(_fwd_ws) > _FWD_WS_KEEP:
-            _fwd_ws.popitem(last=False)
-    else:
-        _fwd_ws.move_to_end(key)
-    return ws, nbytes
-
-
 def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
     """z = relu(pose W1^T + b1) W2^T + b2, (E, 2C), in one launch on the split-bf16 matrix cores
     (``mrp_edge_encoder_fwd_split``); C % 32 != 0 runs on the zero-padded weights
@@ -157,10 +131,8 @@ def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
     z = torch.empty((E, 2 * Cp), device=pose.device, dtype=torch.float32)
     lib = _lib.load_library()
     with torch.cuda.device(pose.device):
-        ws, nb = fwd_workspace(pose.device, E, Cp)
         code = lib.mrp_edge_encoder_fwd_split(_ptr(pose), _ptr(img), _ptr(b2) if b2 is not None else None, E, Cp,
-                                              _ptr(z), _ptr(ws) if ws is not None else None, nb,
-                                              ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream))
+                                              _ptr(z), ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream))
     if code == _lib.HIP_ERROR_NOT_SUPPORTED:
         return None
     _lib.check(code, "mrp_edge_encoder_fwd_split")
@@ -353,10 +325,9 @@ class EdgeEncoderSplitFunction(torch.autograd.Function):
         hT = torch.empty((C, E), device=pose.device, dtype=torch.float32)
         lib = _lib.load_library()
         with torch.cuda.device(pose.device):
-            ws, nb = fwd_workspace(pose.device, E, C)
             _lib.check(lib.mrp_edge_encoder_fwd_split_train(
                 _ptr(pose), _ptr(img), _ptr(b2c) if b2c is not None else None, E, C, _ptr(z), _ptr(hT), E,
-                _ptr(ws) if ws is not None else None, nb, ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
+                ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
         ctx.save_for_backward(pose, w1, b1, w2, b2, hT)
         # W2^T (and its packed image) are built in backward, only for the products that run:
         # a forward whose backward never runs, or runs without dh^T, packs nothing
@@ -535,10 +506,9 @@ class EdgeEncoderPaddedFunction(torch.autograd.Function):
         hT = torch.empty((Cp, Ep), device=dev)
         lib = _lib.load_library()
         with torch.cuda.device(dev):
-            ws, nb = fwd_workspace(dev, Ep, Cp)
             _lib.check(lib.mrp_edge_encoder_fwd_split_train(
                 _ptr(pp), _ptr(rec.img), _ptr(rec.b2), Ep, Cp, _ptr(zp), _ptr(hT), Ep,
-                _ptr(ws) if ws is not None else None, nb, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
+                ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
         ctx.save_for_backward(pp, hT)
         ctx.rec, ctx.E = rec, E
         ctx.has_b2 = b2 is not None

@@ -120,14 +120,14 @@ def test_split_encoder_validation_without_launch():
     assert lib.mrp_edge_encoder_pack_bytes(48) == 0 and lib.mrp_edge_encoder_pack_bytes(0) == 0
     assert lib.mrp_edge_encoder_pack(None, None, None, 48, None, None) == m._lib.HIP_ERROR_NOT_SUPPORTED
     assert lib.mrp_edge_encoder_pack(None, None, None, 64, None, None) == HIP_INVALID_VALUE
-    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 0, 64, None, None, 0, None) == 0  # no edges: no-op
-    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 10, 48, None, None, 0, None) == m._lib.HIP_ERROR_NOT_SUPPORTED
-    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 10, 64, None, None, 0, None) == HIP_INVALID_VALUE
-    assert lib.mrp_edge_encoder_fwd_split(None, None, None, -1, 64, None, None, 0, None) == HIP_INVALID_VALUE
+    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 0, 64, None, None) == 0  # no edges: no-op
+    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 10, 48, None, None) == m._lib.HIP_ERROR_NOT_SUPPORTED
+    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 10, 64, None, None) == HIP_INVALID_VALUE
+    assert lib.mrp_edge_encoder_fwd_split(None, None, None, -1, 64, None, None) == HIP_INVALID_VALUE
     # the image is addressed with 32-bit offsets: 96 C + 12 C^2 bytes must stay below 2^31 (C <= 13344)
     assert 96 * 13344 + 12 * 13344 ** 2 < 2 ** 31 <= 96 * 13376 + 12 * 13376 ** 2
     assert lib.mrp_edge_encoder_pack(None, None, None, 13376, None, None) == m._lib.HIP_ERROR_NOT_SUPPORTED
-    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 10, 13376, None, None, 0, None) == m._lib.HIP_ERROR_NOT_SUPPORTED
+    assert lib.mrp_edge_encoder_fwd_split(None, None, None, 10, 13376, None, None) == m._lib.HIP_ERROR_NOT_SUPPORTED
     assert lib.mrp_edge_encoder_pack(None, None, None, 13344, None, None) == HIP_INVALID_VALUE  # size ok, no pointers
 
 
@@ -137,8 +137,8 @@ def test_split_encoder_training_validation_without_launch():
     lib = m.load_library()
     NS = m._lib.HIP_ERROR_NOT_SUPPORTED
     # forward with h^T: declined shapes, missing pointers
-    assert lib.mrp_edge_encoder_fwd_split_train(None, None, None, 10, 48, None, None, 10, None, 0, None) == NS
-    assert lib.mrp_edge_encoder_fwd_split_train(None, None, None, 32, 64, None, None, 32, None, 0, None) == HIP_INVALID_VALUE
+    assert lib.mrp_edge_encoder_fwd_split_train(None, None, None, 10, 48, None, None, 10, None) == NS
+    assert lib.mrp_edge_encoder_fwd_split_train(None, None, None, 32, 64, None, None, 32, None) == HIP_INVALID_VALUE
     # dz^T: E % 4 and odd C declined; a short row stride is invalid
     assert lib.mrp_edge_encoder_bwd_prep(16, 6, 64, 16, 6, None) == NS
     assert lib.mrp_edge_encoder_bwd_prep(16, 8, 64, 16, 4, None) == HIP_INVALID_VALUE

@@ -224,10 +224,9 @@ def test_train_forward_writes_hidden(cuda_device, E, C):
     z = torch.empty(E, 2 * C, device=cuda_device)
     hT = torch.full((C, E), float("nan"), device=cuda_device)
     lib = m.load_library()
-    ws, nb = m.encoder.fwd_workspace(cuda_device, E, C)
     m._lib.check(lib.mrp_edge_encoder_fwd_split_train(
         _ptr(pose), _ptr(img), _ptr(l2.bias.detach().contiguous()), E, C, _ptr(z), _ptr(hT), E,
-        _ptr(ws) if ws is not None else None, nb, ctypes.c_void_p(torch.cuda.current_stream(cuda_device).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
+        ctypes.c_void_p(torch.cuda.current_stream(cuda_device).cuda_stream)), "mrp_edge_encoder_fwd_split_train")
     with torch.no_grad():
         z_inf = m.encoder.encoder_forward_split(pose, l1, l2)
         h32 = torch.relu(torch.nn.functional.linear(pose, l1.weight, l1.bias)).t()

@@ -42,7 +42,7 @@ for name, E, C in [("head", 1792, 512), ("cfg1", 896, 512), ("cfg2", 1792, 1280)
                 return mrp.encoder.encoder_forward_split(pose, l1, l2)
         lb = _lib._lib
         _lib.check(lb.mrp_edge_encoder_fwd_split_train(
-            _ptr(pose), _ptr(img), _ptr(b2), E, C, _ptr(z), _ptr(hT), E, None, 0,
+            _ptr(pose), _ptr(img), _ptr(b2), E, C, _ptr(z), _ptr(hT), E,
             ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "fwd_split_train")
         return z, hT
     res, outs = {}, {}

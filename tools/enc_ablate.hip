@@ -67,7 +67,6 @@ int main(int argc, char** argv) {
   hipStreamCreate(&st);
   mrp_edge_encoder_pack(w1, b1, w2, C, pk, st);
   FwdArgs a = {};
-  a.ks = 1;
   a.pose = pose;
   a.packed = static_cast<const u4*>(pk);
   a.b2 = b2;

@@ -95,7 +95,7 @@ int main(int argc, char** argv) {
     for (size_t vi = 0; vi < variants.size(); ++vi) {
       CK(mrp_tuning_set("edge_split_v", variants[vi]));
       CK(hipMemset(dz, 0xff, (size_t)E * 2 * C * 4));
-      CK(mrp_edge_encoder_fwd_split(dp, img, db2, E, C, dz, nullptr, 0, st));
+      CK(mrp_edge_encoder_fwd_split(dp, img, db2, E, C, dz, st));
       CK(hipStreamSynchronize(st));
       std::vector<float> h((size_t)E * 2 * C);
       CK(hipMemcpy(h.data(), dz, h.size() * 4, hipMemcpyDeviceToHost));
@@ -104,9 +104,9 @@ int main(int argc, char** argv) {
     for (int r = 0; r < 5; ++r)
       for (size_t vi = 0; vi < variants.size(); ++vi) {
         CK(mrp_tuning_set("edge_split_v", variants[vi]));
-        CK(mrp_edge_encoder_fwd_split(dp, img, db2, E, C, dz, nullptr, 0, st));
+        CK(mrp_edge_encoder_fwd_split(dp, img, db2, E, C, dz, st));
         CK(hipEventRecord(e0, st));
-        for (int i = 0; i < iters; ++i) CK(mrp_edge_encoder_fwd_split(dp, img, db2, E, C, dz, nullptr, 0, st));
+        for (int i = 0; i < iters; ++i) CK(mrp_edge_encoder_fwd_split(dp, img, db2, E, C, dz, st));
         CK(hipEventRecord(e1, st));
         CK(hipEventSynchronize(e1));
         float ms;
