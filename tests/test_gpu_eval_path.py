@@ -124,9 +124,9 @@ def test_split_encoder_column_sums(cuda_device, E, C):
 def test_train_and_eval_encoders_agree(cuda_device, E, C):
     """Train and eval logits of the same weights.  Where E % 32 == 0 (every reference configuration)
     training runs the same split-bf16 kernel (EdgeEncoderSplitFunction), so the two are bit-identical;
-    otherwise training runs mrp_edge_hidden_fwd + the fp32-MFMA mrp_edge_logits_fwd, and then each is
-    within the float64 yardstick, so they differ by at most the sum of two fp32-level errors — stated
-    here, since those two paths are different arithmetic."""
+    otherwise training runs that kernel on zero-padded edges (EdgeEncoderPaddedFunction, possibly in
+    another workgroup form than the unpadded eval launch), and then each is within the float64
+    yardstick, so they differ by at most the sum of two fp32-level errors — stated here."""
     torch.manual_seed(3 * C + E)
     enc = m.edge_encoder([C, C]).to(cuda_device)
     pose = (torch.randn(E, 9) * 8).to(cuda_device)
@@ -137,7 +137,7 @@ def test_train_and_eval_encoders_agree(cuda_device, E, C):
     assert z_train.requires_grad
     assert m.encoder.PATH_COUNTS["split"] == before.get("split", 0) + 1
     split_train = E % 32 == 0
-    key = "split_train" if split_train else "autograd"
+    key = "split_train" if split_train else "split_padded"
     assert m.encoder.PATH_COUNTS[key] == before.get(key, 0) + 1
     if split_train:
         assert torch.equal(z_eval, z_train.detach())
