@@ -38,6 +38,7 @@ import glob
 import json
 import os
 import platform
+import statistics
 import sys
 import time
 import types
@@ -271,21 +272,23 @@ def config0_record(device, args):
     torch.manual_seed(0)
     gcn = mrp.GCN(types.SimpleNamespace(feature_dim=C)).to(device)
     x = g.ndata["image"]
+    # host-bound steps (~50 us of GPU work): the median of three timed runs
     with torch.no_grad():
         for _ in range(10):
             gcn(g, x)
-        t = timed(lambda: gcn(g, x), 50, 1, device, args.dist_backend)
+        t = statistics.median(timed(lambda: gcn(g, x), 50, 1, device, args.dist_backend) for _ in range(3))
     xr = x.detach().clone().requires_grad_(True)
     gy = torch.randn_like(x)
 
     def train():
         for p in gcn.parameters():
             p.grad = None
+        xr.grad = None  # the layer's input is the backbone's output in the reference: never accumulated
         gcn(g, xr).backward(gy)
 
     for _ in range(5):
         train()
-    tt = timed(train, 20, 1, device, args.dist_backend)
+    tt = statistics.median(timed(train, 20, 1, device, args.dist_backend) for _ in range(3))
     rec = {"config": "configs[0]: 4-robot complete graph, random 64x32x32 node feats, 1 GraphConv layer, "
                      "DGL CPU backend (dgl/training.py plumbing)",
            "graphs": B, "robots": N, "channels": C, "H": H, "W": H, "layers": 1,
