@@ -4,8 +4,11 @@ the HIP backward kernels writing straight into the bucket slots, and ``shard_gra
 the reduced gradients of a 2-layer GCN stack on a sharded batch against the single-rank full-batch
 gradients (the reference's data parallelism: ``dgl/training.py:324-325``).
 
-RCCL cannot place two ranks on one GPU, so the test needs two: on a one-GPU box it skips, saying so.
-The CPU suite runs the same path over gloo (``tests/test_dist_gloo.py``)."""
+RCCL cannot place two ranks on one GPU, so that test needs two: on a one-GPU box it skips, saying so.
+The single-rank test runs everywhere: an RCCL communicator of one rank, the reducer's pre-multiplied
+sum (``dist._make_nccl_premul_sum``) launched on every bucket over the GPU, the gradients scaled by the
+rank's share exactly as the collective defines it — the RCCL code path of ``bench.py --gpus N``'s
+training records, executed.  The CPU suite runs the same path over gloo (``tests/test_dist_gloo.py``)."""
 import os
 import socket
 import types
@@ -21,6 +24,62 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _single(rank, port, out):
+    import torch.distributed as dist
+
+    import mrp_gnn_amd as m
+    from mrp_gnn_amd.dist import GradAllReducer
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        B, N, C, H = 3, 8, 64, 8
+        rng = np.random.RandomState(9)
+        frames = []
+        for _ in range(B):
+            poses = np.concatenate([rng.uniform(-5, 5, (N, 3)), rng.standard_normal((N, 4))], 1).astype(np.float32)
+            f = m.frame_graph(poses)
+            f.ndata["image"] = torch.from_numpy(rng.standard_normal((N, C, H, H)).astype(np.float32))
+            frames.append(f)
+        g = m.batch(frames).to(dev)
+        opt = types.SimpleNamespace(feature_dim=C, compress_gcn=True, multi_gcn=False, gcn_layers=2,
+                                    gcn_combine="cat_compress")
+        torch.manual_seed(0)
+        ref = m.GCNStack(opt).to(dev)
+        ref(g, g.ndata["image"]).square().mean().backward()
+        torch.manual_seed(0)
+        model = m.GCNStack(opt).to(dev)
+        red = GradAllReducer(model.parameters(), bucket_bytes=1 << 16)
+        red.set_local_count(2)
+        red._scale = 0.25  # as if other ranks held 6 more graphs: the collective must scale by 2 / 8
+        model(g, g.ndata["image"]).square().mean().backward()
+        red.synchronize()
+        errs = {}
+        for (k, p), q in zip(model.named_parameters(), ref.parameters()):
+            errs[k] = float((p.grad - 0.25 * q.grad).abs().max() / q.grad.abs().max().clamp_min(1e-30))
+        out[0] = {"errs": errs, "buckets": len(red.buckets), "premul": red.scaled_passes_skipped,
+                  "backend": dist.get_backend()}
+        red.remove()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_single_rank_premul_sum():
+    """One RCCL rank: every bucket's all-reduce is the pre-multiplied sum on the GPU, the gradients come
+    back scaled by the rank's share (2 of 8 graphs: 1/4) and otherwise bit-identical to no reducer."""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_single, args=(_free_port(), out), nprocs=1, join=True)
+    rec = out[0]
+    assert rec["backend"] == "nccl"
+    assert rec["premul"] >= rec["buckets"] >= 1, rec
+    for k, e in rec["errs"].items():
+        assert e == 0.0, (k, e)  # x * 0.25 is exact in fp32
 
 
 def _worker(rank, world, port, out):
