@@ -80,6 +80,7 @@ def clear_packed_weights() -> None:
     _w2t_cache.clear()
     _w2t_img_cache.clear()
     _padded.clear()
+    _ready.clear()
 
 
 def _pack(w1, b1, w2) -> torch.Tensor:
@@ -104,39 +105,125 @@ def packed_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> torch.Tensor:
         return hit[1]
     img = _pack(w1, b1, w2)
     _packed[l2] = (key, img)
+    _track_image(img)
     return img
+
+
+# The inference encoder on its own stream (one per device), ordered after the producers of what it
+# reads rather than after everything queued before it: its inputs — the poses, b2 and the packed
+# weight image — each carry the event recorded on the caller's stream when this module first saw them
+# in their current state (tensor object and autograd version; the image: when it was packed), and the
+# caller's stream waits for the encoder before the aggregation that reads its logits.  So the encoder
+# of a batch whose inputs are ready runs beside the aggregation of the previous batch (an HBM-bound
+# kernel) instead of after it.  Every write to those inputs that bumps the version counter is ordered
+# (a new event); writes that bypass it (``.data``, foreign kernels) need ``clear_packed_weights()``, as
+# for the packed images.  Not under stream capture (one stream there).  set_encoder_stream(False):
+# the caller's stream.
+_ENC_STREAM = True
+_enc_streams = {}
+_ready = {}        # id(tensor) -> (weakref, version, event)
+_image_ready = {}  # id(packed image) -> (weakref, event recorded after its pack kernel)
+
+
+def set_encoder_stream(on: bool) -> None:
+    global _ENC_STREAM
+    _ENC_STREAM = bool(on)
+
+
+def _record(dev: torch.device) -> torch.cuda.Event:
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    return ev
+
+
+def _track_image(img: torch.Tensor) -> None:
+    """The event after a packed image's pack kernel (dropped with the image)."""
+    iid = id(img)
+    _image_ready[iid] = (weakref.ref(img, lambda _r, iid=iid: _image_ready.pop(iid, None)), _record(img.device))
+
+
+def _ready_event(t: torch.Tensor) -> torch.cuda.Event:
+    """The event after which ``t`` (in its current version) is complete on the caller's stream."""
+    hit = _ready.get(id(t))
+    if hit is not None and hit[0]() is t and hit[1] == t._version:
+        return hit[2]
+    ev = _record(t.device)
+    tid = id(t)
+    _ready[tid] = (weakref.ref(t, lambda _r, tid=tid: _ready.pop(tid, None)), t._version, ev)
+    return ev
+
+
+def _enc_stream(dev: torch.device) -> torch.cuda.Stream:
+    s = _enc_streams.get(dev.index)
+    if s is None:
+        s = _enc_streams[dev.index] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
     """z = relu(pose W1^T + b1) W2^T + b2, (E, 2C), in one launch on the split-bf16 matrix cores
-    (``mrp_edge_encoder_fwd_split``); C % 32 != 0 runs on the zero-padded weights
-    (:func:`padded_weights`) and keeps z's 2C leading columns.  None when no weight image exists for
-    the shape (C beyond ``mrp_edge_encoder_pack``'s bound, layers not the reference's)."""
+    (``mrp_edge_encoder_fwd_split``), on the encoder stream (see above); C % 32 != 0 runs on the
+    zero-padded weights (:func:`padded_weights`) and keeps z's 2C leading columns.  None when no
+    weight image exists for the shape (C beyond ``mrp_edge_encoder_pack``'s bound, layers not the
+    reference's)."""
     C = l1.weight.shape[0]
     if not pose.is_cuda:
         raise RuntimeError("mrp_gnn: the edge encoder kernel runs only on the GPU; no CPU fallback")
     if tuple(l1.weight.shape) != (C, 9) or tuple(l2.weight.shape) != (2 * C, C) or l1.bias is None or C == 0:
         return None
+    # readiness is tracked on the tensors the caller holds (detach() makes a new tensor object per call,
+    # sharing the version counter)
     if C % 32 == 0 and image_supported(C):
         img = packed_weights(l1, l2)
         b2 = l2.bias.detach().contiguous().float() if l2.bias is not None else None
+        b2_src = l2.bias
         Cp = C
     elif image_supported(_pad32(C)):
         rec = padded_weights(l1, l2)
         img, b2, Cp = rec.img, rec.b2, rec.Cp
+        b2_src = b2
     else:
         return None
+    pose_src = pose
     pose = pose.detach().contiguous().float()
     E = pose.shape[0]
-    z = torch.empty((E, 2 * Cp), device=pose.device, dtype=torch.float32)
+    dev = pose.device
+    cur = torch.cuda.current_stream(dev)
+    side = None
+    if _ENC_STREAM and not torch.cuda.is_current_stream_capturing():
+        side = _enc_stream(dev)
+        for src, t in ((pose_src, pose), (b2_src, b2)):
+            if t is None:
+                continue
+            # a converted copy (non-contiguous or non-fp32 input) was made just now on the caller's stream
+            same = src is not None and t.data_ptr() == src.data_ptr() and t.dtype == src.dtype
+            side.wait_event(_ready_event(src) if same else _record(dev))
+        hit = _image_ready.get(id(img))
+        if hit is not None and hit[0]() is img:
+            side.wait_event(hit[1])
+        else:  # an image packed before this module tracked it: after everything queued so far
+            side.wait_stream(cur)
+    run = side if side is not None else cur
     lib = _lib.load_library()
-    with torch.cuda.device(pose.device):
+    with torch.cuda.device(dev), torch.cuda.stream(run):
+        z = torch.empty((E, 2 * Cp), device=dev, dtype=torch.float32)
         code = lib.mrp_edge_encoder_fwd_split(_ptr(pose), _ptr(img), _ptr(b2) if b2 is not None else None, E, Cp,
-                                              _ptr(z), ctypes.c_void_p(torch.cuda.current_stream(pose.device).cuda_stream))
-    if code == _lib.HIP_ERROR_NOT_SUPPORTED:
-        return None
-    _lib.check(code, "mrp_edge_encoder_fwd_split")
-    return z if Cp == C else z[:, : 2 * C].contiguous()
+                                              _ptr(z), ctypes.c_void_p(run.cuda_stream))
+        if code == _lib.HIP_ERROR_NOT_SUPPORTED:
+            return None
+        _lib.check(code, "mrp_edge_encoder_fwd_split")
+        if Cp != C:
+            z = z[:, : 2 * C].contiguous()
+    if side is not None:
+        # the caller's stream (and whatever it runs next: the aggregation, an optimizer step writing the
+        # weights) waits for the encoder; the tensors the encoder read or wrote are not recycled by the
+        # caching allocator before both streams are past them
+        cur.wait_stream(side)
+        z.record_stream(cur)
+        for t in (pose, img, b2):
+            if t is not None:
+                t.record_stream(side)
+    return z
 
 
 def logits_forward(h, w2, b2) -> torch.Tensor:
@@ -479,6 +566,7 @@ def padded_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> "_PaddedWeights"
         if b2 is not None:
             r.b2[: 2 * C] = b2
     r.img = _pack(r.w1, r.b1, r.w2)
+    _track_image(r.img)
     _padded[l2] = r
     return r
 

@@ -152,3 +152,65 @@ def test_train_and_eval_encoders_agree(cuda_device, E, C):
         assert ok, errs
     diff = stack_ref.err(z_eval, z_train.detach()) * float(z_train.abs().max()) / float(z64.abs().max())
     assert diff <= 2 * max(1e-5, 4.0 * e_f32), (diff, e_f32)
+
+
+def _forward(gcn, g, x, own_stream):
+    m.encoder.set_encoder_stream(own_stream)
+    try:
+        with torch.no_grad():
+            return gcn(g, x).clone()
+    finally:
+        m.encoder.set_encoder_stream(True)
+
+
+def test_encoder_stream_ordered_after_input_writes(cuda_device):
+    """The inference encoder runs on its own stream (``encoder.set_encoder_stream``, the default), ordered
+    after the producers of what it reads, not after everything queued before it.  Its results are the
+    caller's-stream results bit for bit; in-place writes to the poses and to the weights (an optimizer
+    step), queued behind long kernels on the caller's stream, are seen by the next forward; and under
+    stream capture the layer records on one stream and replays to the same bits."""
+    C = 64
+    g = _headline_graph(cuda_device, B=6, C=C, H=16)
+    torch.manual_seed(2)
+    gcn = m.GCN(types.SimpleNamespace(feature_dim=C)).to(cuda_device)
+    x = g.ndata["image"]
+    a, b = _forward(gcn, g, x, True), _forward(gcn, g, x, False)
+    assert torch.equal(a, b)
+    busy = torch.randn(64 << 20, device=cuda_device)  # 256 MB: keeps the caller's stream busy
+
+    def stall():
+        for _ in range(4):
+            busy.mul_(1.0)
+
+    # poses written in place (a version bump) behind the stall
+    pose = g.edata["pose"]
+    with torch.no_grad():
+        stall()
+        pose.mul_(1.25)
+    c = _forward(gcn, g, x, True)
+    assert torch.equal(c, _forward(gcn, g, x, False)) and not torch.equal(c, a)
+    # every weight updated in place behind the stall, as an optimizer step would
+    with torch.no_grad():
+        stall()
+        for p in gcn.parameters():
+            p.mul_(0.75)
+    d = _forward(gcn, g, x, True)
+    assert torch.equal(d, _forward(gcn, g, x, False)) and not torch.equal(d, c)
+    # only b2 changed: it is not in the packed image's key, its own readiness event orders it
+    with torch.no_grad():
+        stall()
+        gcn.edge_encoder.layers[2].bias.add_(0.5)
+    e = _forward(gcn, g, x, True)
+    assert torch.equal(e, _forward(gcn, g, x, False)) and not torch.equal(e, d)
+    # stream capture: one stream, replayed
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.stream(side):
+        gcn(g, x)  # warm the allocator and the packed image outside the capture
+        torch.cuda.current_stream().synchronize()
+        with torch.cuda.graph(graph, stream=side):
+            out = gcn(g, x)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, e)
