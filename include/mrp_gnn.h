@@ -443,7 +443,7 @@ int mrp_frame_graph_build(const float* poses, int32_t num_graphs, int32_t n, int
 int mrp_tuning_set(const char* name, int32_t value);
 
 /* Library identification: ABI version (incremented on signature changes; 21 = this header: v19 plus
- * the streaming yardstick mrp_stream_copy and the encoder's pose gradient (mrp_edge_encoder_bwd_pose
+ * the streaming yardstick mrp_stream_copy, the device-scope stream join mrp_stream_join and the encoder's pose gradient (mrp_edge_encoder_bwd_pose
  * + workspace); 20: v19 plus a one-launch no-grad GCN layer
  * (mrp_gcn_fwd_fused), measured slower than the two launches it replaced and removed in 21
  * (tools/lab_patches/r06_fused_layer.patch); 19: v18 with
@@ -468,6 +468,12 @@ int mrp_abi_version(void);
  * and store per thread — the 1-read-1-write copy the HBM-bound kernels are measured against on the
  * same box in the same run.  Not part of the GCN path. */
 int mrp_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);
+
+/* Stream join: work enqueued on `waiter` after this call waits for everything enqueued on `signaller`
+ * before it — an event recorded with a device-scope release (no system-scope cache writeback: the
+ * joined work is on the same device) that `waiter` waits on.  The inference encoder's stream joins the
+ * caller's stream with it (encoder.py).  Returns a hipError_t. */
+int mrp_stream_join(void* waiter, void* signaller);
 
 /* Human-readable text for a return code (static storage). */
 const char* mrp_error_string(int code);

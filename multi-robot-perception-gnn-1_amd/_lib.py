@@ -55,6 +55,7 @@ EXPORTED_SYMBOLS = (
     "mrp_edge_encoder_bwd_pose",
     "mrp_frame_graph_build",
     "mrp_stream_copy",
+    "mrp_stream_join",
     "mrp_tuning_set",
     "mrp_abi_version",
     "mrp_error_string",
@@ -174,6 +175,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mrp_frame_graph_build.restype = ctypes.c_int
     lib.mrp_stream_copy.argtypes = [_P, _P, _I64, _P]
     lib.mrp_stream_copy.restype = ctypes.c_int
+    lib.mrp_stream_join.argtypes = [_P, _P]
+    lib.mrp_stream_join.restype = ctypes.c_int
     lib.mrp_abi_version.argtypes = []
     lib.mrp_abi_version.restype = ctypes.c_int
     lib.mrp_error_string.argtypes = [ctypes.c_int]

@@ -139,6 +139,17 @@ int mrp_tuning_set(const char* name, int32_t value) {
 
 const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hipError_t>(code)); }
 
+int mrp_stream_join(void* waiter, void* signaller) {
+  if (waiter == signaller) return hipSuccess;
+  hipEvent_t ev;
+  hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice);
+  if (e != hipSuccess) return e;
+  e = hipEventRecord(ev, static_cast<hipStream_t>(signaller));
+  if (e == hipSuccess) e = hipStreamWaitEvent(static_cast<hipStream_t>(waiter), ev, 0);
+  const hipError_t d = hipEventDestroy(ev);  // released once the wait has consumed it
+  return e != hipSuccess ? e : d;
+}
+
 int mrp_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
   if (bytes < 0 || (bytes % 16) != 0) return hipErrorInvalidValue;
   if (bytes == 0) return hipSuccess;

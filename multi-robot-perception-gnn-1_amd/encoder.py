@@ -153,10 +153,31 @@ def _ready_event(t: torch.Tensor) -> torch.cuda.Event:
     return ev
 
 
+_ENC_PRIORITY = -1  # the highest the runtime offers (torch: lower is higher); 0 = normal
+# the caller's stream joins the encoder's through a device-scope event (mrp_stream_join) instead of
+# torch's wait_stream, whose event carries a system-scope release (False: torch's, lab A/B)
+_FAST_JOIN = True
+
+
+def set_fast_join(on: bool) -> None:
+    global _FAST_JOIN
+    _FAST_JOIN = bool(on)
+
+
+def set_encoder_stream_priority(priority: int) -> None:
+    """Priority of the encoder stream (lab A/B): at normal priority its workgroups queue behind the
+    aggregation's thousands and it finishes late; high priority lets it through first."""
+    global _ENC_PRIORITY
+    _ENC_PRIORITY = int(priority)
+    _enc_streams.clear()
+
+
 def _enc_stream(dev: torch.device) -> torch.cuda.Stream:
     s = _enc_streams.get(dev.index)
     if s is None:
-        s = _enc_streams[dev.index] = torch.cuda.Stream(device=dev)
+        lo, hi = torch.cuda.Stream.priority_range()  # (lowest, highest), e.g. (0, -1)
+        prio = max(min(_ENC_PRIORITY, lo), hi)
+        s = _enc_streams[dev.index] = torch.cuda.Stream(device=dev, priority=prio)
     return s
 
 
@@ -218,7 +239,11 @@ def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
         # the caller's stream (and whatever it runs next: the aggregation, an optimizer step writing the
         # weights) waits for the encoder; the tensors the encoder read or wrote are not recycled by the
         # caching allocator before both streams are past them
-        cur.wait_stream(side)
+        if _FAST_JOIN:
+            _lib.check(lib.mrp_stream_join(ctypes.c_void_p(cur.cuda_stream), ctypes.c_void_p(side.cuda_stream)),
+                       "mrp_stream_join")
+        else:
+            cur.wait_stream(side)
         z.record_stream(cur)
         for t in (pose, img, b2):
             if t is not None:

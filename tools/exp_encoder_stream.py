@@ -1,6 +1,6 @@
 """Kernel lab (not product code): the headline step (bench.py's no-grad GCN.forward, B = 32, N = 8, C = 512,
 32 x 32) with the inference encoder on its own stream (``encoder.set_encoder_stream(True)``, the default)
-against the caller's stream, timed like bench.py, settings interleaved over rounds; outputs compared.
+at normal and high priority, against the caller's stream, timed like bench.py, settings interleaved over rounds; outputs compared.
 usage: python tools/exp_encoder_stream.py [steps] [rounds]"""
 import os
 import sys
@@ -27,9 +27,13 @@ with torch.no_grad():
         for _ in range(20):
             gcn(g, x)
         torch.cuda.synchronize()
+    # (own stream, priority, device-scope join)
+    settings = [(False, 0, True), (True, 0, False), (True, -1, False), (True, 0, True), (True, -1, True)]
     for rnd in range(rounds):
-        for on in (False, True):
+        for on, prio, fj in settings:
             mrp.encoder.set_encoder_stream(on)
+            mrp.encoder.set_encoder_stream_priority(prio)
+            mrp.encoder.set_fast_join(fj)
             for _ in range(10):
                 gcn(g, x)
             torch.cuda.synchronize()
@@ -37,10 +41,12 @@ with torch.no_grad():
             for _ in range(steps):
                 out = gcn(g, x)
             torch.cuda.synchronize()
-            res.setdefault(on, []).append((time.perf_counter() - t) / steps * 1e6)
-            outs[on] = out.clone()
+            res.setdefault((on, prio, fj), []).append((time.perf_counter() - t) / steps * 1e6)
+            outs[(on, prio, fj)] = out.clone()
 mrp.encoder.set_encoder_stream(True)
-for on, ts in res.items():
-    print(f"encoder stream {'own' if on else 'caller'}: " + " ".join(f"{t:6.1f}" for t in ts) +
-          f"  min {min(ts):6.1f} us/step", flush=True)
-print("outputs bit-identical:", torch.equal(outs[True], outs[False]))
+mrp.encoder.set_encoder_stream_priority(-1)
+mrp.encoder.set_fast_join(True)
+for (on, prio, fj), ts in res.items():
+    print(f"encoder stream {'own' if on else 'caller'} priority {prio} join {'device' if fj else 'torch'}: "
+          + " ".join(f"{t:6.1f}" for t in ts) + f"  min {min(ts):6.1f} us/step", flush=True)
+print("outputs bit-identical:", all(torch.equal(o, outs[settings[0]]) for o in outs.values()))
