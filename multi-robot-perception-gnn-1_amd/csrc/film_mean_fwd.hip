@@ -1,6 +1,7 @@
 // film_mean_fwd.hip — forward launchers and C ABI (mrp_film_mean_fwd, mrp_film_mean_cat_fwd).
 // Kernels and design notes: film_mean_kernels.hpp.
 #include <cstring>
+#include <unordered_map>
 
 #include "film_mean_kernels.hpp"
 
@@ -141,13 +142,20 @@ const char* mrp_error_string(int code) { return hipGetErrorString(static_cast<hi
 
 int mrp_stream_join(void* waiter, void* signaller) {
   if (waiter == signaller) return hipSuccess;
-  hipEvent_t ev;
-  hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice);
-  if (e != hipSuccess) return e;
-  e = hipEventRecord(ev, static_cast<hipStream_t>(signaller));
+  // one event per signalling stream and host thread, re-recorded each call: a wait enqueued earlier
+  // keeps the record it was enqueued behind
+  thread_local std::unordered_map<void*, hipEvent_t> events;
+  hipEvent_t& ev = events[signaller];
+  if (ev == nullptr) {
+    const hipError_t c = hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice);
+    if (c != hipSuccess) {
+      ev = nullptr;
+      return c;
+    }
+  }
+  hipError_t e = hipEventRecord(ev, static_cast<hipStream_t>(signaller));
   if (e == hipSuccess) e = hipStreamWaitEvent(static_cast<hipStream_t>(waiter), ev, 0);
-  const hipError_t d = hipEventDestroy(ev);  // released once the wait has consumed it
-  return e != hipSuccess ? e : d;
+  return e;
 }
 
 int mrp_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import collections
 import ctypes
+import os
 import weakref
 
 import torch
@@ -119,8 +120,13 @@ def packed_weights(l1: torch.nn.Linear, l2: torch.nn.Linear) -> torch.Tensor:
 # (a new event); writes that bypass it (``.data``, foreign kernels) need ``clear_packed_weights()``, as
 # for the packed images.  Not under stream capture (one stream there).  set_encoder_stream(False):
 # the caller's stream.
-_ENC_STREAM = True
+_ENC_STREAM = os.environ.get("MRP_ENCODER_STREAM", "1") != "0"
+# below this many E x C products the encoder is a few microseconds of GPU work and the stream's
+# bookkeeping (its waits and the join, ~10 us of host time) would cost more than the overlap saves
+_ENC_STREAM_MIN_WORK = 1 << 18
 _enc_streams = {}
+_waited = {}       # device index -> ids of readiness events the encoder stream already waits behind
+_recorded = {}     # device index -> {id(tensor): weakref} already recorded on the encoder stream
 _ready = {}        # id(tensor) -> (weakref, version, event)
 _image_ready = {}  # id(packed image) -> (weakref, event recorded after its pack kernel)
 
@@ -211,17 +217,28 @@ def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
     dev = pose.device
     cur = torch.cuda.current_stream(dev)
     side = None
-    if _ENC_STREAM and not torch.cuda.is_current_stream_capturing():
+    if _ENC_STREAM and E * C >= _ENC_STREAM_MIN_WORK and not torch.cuda.is_current_stream_capturing():
         side = _enc_stream(dev)
+        waited = _waited.setdefault(dev.index, {})
+
+        def wait(ev):
+            # the encoder stream's waits are in its own order: one it already passed need not be repeated
+            if waited.get(id(ev)) is not ev:
+                side.wait_event(ev)
+                waited[id(ev)] = ev
+                if len(waited) > 64:
+                    waited.clear()
+                    waited[id(ev)] = ev
+
         for src, t in ((pose_src, pose), (b2_src, b2)):
             if t is None:
                 continue
             # a converted copy (non-contiguous or non-fp32 input) was made just now on the caller's stream
             same = src is not None and t.data_ptr() == src.data_ptr() and t.dtype == src.dtype
-            side.wait_event(_ready_event(src) if same else _record(dev))
+            wait(_ready_event(src) if same else _record(dev))
         hit = _image_ready.get(id(img))
         if hit is not None and hit[0]() is img:
-            side.wait_event(hit[1])
+            wait(hit[1])
         else:  # an image packed before this module tracked it: after everything queued so far
             side.wait_stream(cur)
     run = side if side is not None else cur
@@ -245,9 +262,14 @@ def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
         else:
             cur.wait_stream(side)
         z.record_stream(cur)
-        for t in (pose, img, b2):
+        rec = _recorded.setdefault(dev.index, {})
+        for t in (pose_src if pose.data_ptr() == pose_src.data_ptr() else pose, img, b2):
             if t is not None:
-                t.record_stream(side)
+                hit = rec.get(id(t))
+                if hit is None or hit() is not t:  # the block keeps its recorded streams for its lifetime
+                    t.record_stream(side)
+                    tid = id(t)
+                    rec[tid] = weakref.ref(t, lambda _r, tid=tid, rec=rec: rec.pop(tid, None))
     return z
 
 
