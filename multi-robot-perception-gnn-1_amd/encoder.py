@@ -136,20 +136,6 @@ def set_encoder_stream(on: bool) -> None:
     _ENC_STREAM = bool(on)
 
 
-_LAYER_OVERLAP = os.environ.get("MRP_LAYER_STREAMS", "1") != "0"
-
-
-def set_layer_overlap(on: bool) -> None:
-    """No-grad GCN layers on alternating layer streams (``layer_stream``; default on) or the caller's
-    stream with only the encoder on its own (off)."""
-    global _LAYER_OVERLAP
-    _LAYER_OVERLAP = bool(on)
-
-
-def layer_overlap_enabled() -> bool:
-    return _LAYER_OVERLAP and _ENC_STREAM
-
-
 def _record(dev: torch.device) -> torch.cuda.Event:
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
@@ -190,24 +176,6 @@ def set_encoder_stream_priority(priority: int) -> None:
     global _ENC_PRIORITY
     _ENC_PRIORITY = int(priority)
     _enc_streams.clear()
-    _layer_streams.clear()
-
-
-_layer_streams = {}
-
-
-def layer_stream(dev: torch.device) -> torch.cuda.Stream:
-    """The next of two streams (round robin, per device) a whole no-grad GCN layer — encoder and
-    aggregation — runs on (models.GCN.forward): consecutive batches' layers alternate, so one batch's
-    encoder runs beside the previous batch's aggregation with no cross-stream wait in front of either
-    kernel; the caller's stream joins each layer's stream after it."""
-    ent = _layer_streams.get(dev.index)
-    if ent is None:
-        lo, hi = torch.cuda.Stream.priority_range()
-        prio = max(min(_ENC_PRIORITY, lo), hi)
-        ent = _layer_streams[dev.index] = [[torch.cuda.Stream(device=dev, priority=prio) for _ in range(2)], 0]
-    ent[1] ^= 1
-    return ent[0][ent[1]]
 
 
 def _enc_stream(dev: torch.device) -> torch.cuda.Stream:
@@ -219,15 +187,19 @@ def _enc_stream(dev: torch.device) -> torch.cuda.Stream:
     return s
 
 
-def encoder_operands(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
-    """(reads, img, b2, C, Cp) of the inference launch — ``reads`` the (caller's tensor, tensor the
-    kernel reads) pairs of the poses and b2, the packed (or zero-padded, Cp = C rounded up to 32) weight
-    image — or None when no weight image exists for the shape."""
+def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
+    """z = relu(pose W1^T + b1) W2^T + b2, (E, 2C), in one launch on the split-bf16 matrix cores
+    (``mrp_edge_encoder_fwd_split``), on the encoder stream (see above); C % 32 != 0 runs on the
+    zero-padded weights (:func:`padded_weights`) and keeps z's 2C leading columns.  None when no
+    weight image exists for the shape (C beyond ``mrp_edge_encoder_pack``'s bound, layers not the
+    reference's)."""
     C = l1.weight.shape[0]
     if not pose.is_cuda:
         raise RuntimeError("mrp_gnn: the edge encoder kernel runs only on the GPU; no CPU fallback")
     if tuple(l1.weight.shape) != (C, 9) or tuple(l2.weight.shape) != (2 * C, C) or l1.bias is None or C == 0:
         return None
+    # readiness is tracked on the tensors the caller holds (detach() makes a new tensor object per call,
+    # sharing the version counter)
     if C % 32 == 0 and image_supported(C):
         img = packed_weights(l1, l2)
         b2 = l2.bias.detach().contiguous().float() if l2.bias is not None else None
@@ -239,57 +211,35 @@ def encoder_operands(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
         b2_src = b2
     else:
         return None
-    # readiness is tracked on the tensors the caller holds (detach() makes a new tensor object per call,
-    # sharing the version counter)
-    return ((pose, pose.detach().contiguous().float()), (b2_src, b2)), img, b2, C, Cp
-
-
-def launch_encoder(ops, stream) -> torch.Tensor:
-    """The inference launch of :func:`encoder_operands`' operands on ``stream`` (the current device's);
-    z (E, 2C) allocated on it.  None if the kernel declines."""
-    reads, img, b2, C, Cp = ops
-    pose = reads[0][1]
+    pose_src = pose
+    pose = pose.detach().contiguous().float()
     E = pose.shape[0]
+    dev = pose.device
+    cur = torch.cuda.current_stream(dev)
+    side = _enc_begin(dev, E * C, ((pose_src, pose), (b2_src, b2)), img)
+    run = side if side is not None else cur
     lib = _lib.load_library()
-    with torch.cuda.device(pose.device), torch.cuda.stream(stream):
-        z = torch.empty((E, 2 * Cp), device=pose.device, dtype=torch.float32)
+    with torch.cuda.device(dev), torch.cuda.stream(run):
+        z = torch.empty((E, 2 * Cp), device=dev, dtype=torch.float32)
         code = lib.mrp_edge_encoder_fwd_split(_ptr(pose), _ptr(img), _ptr(b2) if b2 is not None else None, E, Cp,
-                                              _ptr(z), ctypes.c_void_p(stream.cuda_stream))
+                                              _ptr(z), ctypes.c_void_p(run.cuda_stream))
         if code == _lib.HIP_ERROR_NOT_SUPPORTED:
             return None
         _lib.check(code, "mrp_edge_encoder_fwd_split")
         if Cp != C:
             z = z[:, : 2 * C].contiguous()
-    PATH_COUNTS["split"] += 1
+    _enc_end(dev, side, (z,), ((pose_src, pose), (None, img), (None, b2)))
     return z
 
 
-def encoder_forward_split(pose, l1: torch.nn.Linear, l2: torch.nn.Linear):
-    """z = relu(pose W1^T + b1) W2^T + b2, (E, 2C), in one launch on the split-bf16 matrix cores
-    (``mrp_edge_encoder_fwd_split``), on the encoder stream (see above); C % 32 != 0 runs on the
-    zero-padded weights (:func:`padded_weights`) and keeps z's 2C leading columns.  None when no
-    weight image exists for the shape (C beyond ``mrp_edge_encoder_pack``'s bound, layers not the
-    reference's)."""
-    ops = encoder_operands(pose, l1, l2)
-    if ops is None:
-        return None
-    reads, img, _b2, C, _Cp = ops
-    dev = pose.device
-    side = _enc_begin(dev, pose.shape[0] * C, reads, img)
-    z = launch_encoder(ops, side if side is not None else torch.cuda.current_stream(dev))
-    if z is not None:
-        _enc_end(dev, side, (z,), reads + ((None, img),))
-    return z
-
-
-def _enc_begin(dev: torch.device, work: int, reads, img, side=None):
-    """The stream the encoder runs on: its own (or ``side``), after the readiness events of ``reads``
-    ((caller's tensor, tensor the kernel reads) pairs) and of the packed image; or None for the caller's
-    stream (small encoders, stream capture, set_encoder_stream(False))."""
+def _enc_begin(dev: torch.device, work: int, reads, img):
+    """The stream the encoder runs on: its own, after the readiness events of ``reads`` ((caller's
+    tensor, tensor the kernel reads) pairs) and of the packed image; or None for the caller's stream
+    (small encoders, stream capture, set_encoder_stream(False))."""
     if not _ENC_STREAM or work < _ENC_STREAM_MIN_WORK or torch.cuda.is_current_stream_capturing():
         return None
-    side = side if side is not None else _enc_stream(dev)
-    waited = _waited.setdefault(side.cuda_stream, {})
+    side = _enc_stream(dev)
+    waited = _waited.setdefault(dev.index, {})
 
     def wait(ev):
         # the encoder stream's waits are in its own order: one it already passed need not be repeated
@@ -306,12 +256,11 @@ def _enc_begin(dev: torch.device, work: int, reads, img, side=None):
         # a converted copy (non-contiguous or non-fp32 input) was made just now on the caller's stream
         same = src is not None and t.data_ptr() == src.data_ptr() and t.dtype == src.dtype
         wait(_ready_event(src) if same else _record(dev))
-    if img is not None:
-        hit = _image_ready.get(id(img))
-        if hit is not None and hit[0]() is img:
-            wait(hit[1])
-        else:  # an image packed before this module tracked it: after everything queued so far
-            side.wait_stream(torch.cuda.current_stream(dev))
+    hit = _image_ready.get(id(img))
+    if hit is not None and hit[0]() is img:
+        wait(hit[1])
+    else:  # an image packed before this module tracked it: after everything queued so far
+        side.wait_stream(torch.cuda.current_stream(dev))
     return side
 
 
@@ -329,7 +278,7 @@ def _enc_end(dev: torch.device, side, outs, reads) -> None:
         cur.wait_stream(side)
     for t in outs:
         t.record_stream(cur)
-    rec = _recorded.setdefault(side.cuda_stream, {})
+    rec = _recorded.setdefault(dev.index, {})
     for src, t in reads:
         if t is None:
             continue
@@ -749,8 +698,9 @@ def edge_logits(enc_layers: torch.nn.Sequential, pose: torch.Tensor) -> torch.Te
     params = (pose, l1.weight, l1.bias, l2.weight, l2.bias)
     inference = not (torch.is_grad_enabled() and any(t.requires_grad for t in params))
     if _LOGITS_PATH == "split" and inference:
-        z = encoder_forward_split(pose, l1, l2)  # counted in PATH_COUNTS["split"] by its launch
+        z = encoder_forward_split(pose, l1, l2)
         if z is not None:
+            PATH_COUNTS["split"] += 1
             return z
     C, E = l1.weight.shape[0], pose.shape[0]
     if _LOGITS_PATH == "split" and l1.bias is not None and tuple(l1.weight.shape) == (C, 9) \

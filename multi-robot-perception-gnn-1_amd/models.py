@@ -35,8 +35,7 @@ import torch.nn as nn
 
 from .aggregate import film_mean, film_mean_cat, film_mean_mix, film_mean_residual
 from .compress import compress_1x1, compress_path, film_compress, film_compress_supported
-from .encoder import edge_logits, encoder_operands, launch_encoder, layer_stream
-from .encoder import _enc_begin as enc_begin, _enc_end as enc_end, layer_overlap_enabled
+from .encoder import edge_logits
 
 
 def clear_packed_weights() -> None:
@@ -143,43 +142,9 @@ class GCN(_PackedImages, nn.Module):
         mode = _opt(self.opt, "gcn_mode", "film_mean")
         if mode == "copy_mean":
             return film_mean(x, None, g.csr(x.device), mode)
-        if mode == "film_mean" and x.is_cuda and layer_overlap_enabled() and not (torch.is_grad_enabled() and (
-                x.requires_grad or any(p.requires_grad for p in self.edge_encoder.parameters()))):
-            out = self._forward_on_layer_stream(g, x)
-            if out is not None:
-                return out
         # logits in, sigmoid applied inside the aggregation kernel
         z = self.edge_encoder.logits(g.edata["pose"])
         return film_mean(x, z, g.csr(x.device), mode, logits=True)
-
-    def _forward_on_layer_stream(self, g, x):
-        """No gradient wanted: encoder + aggregation of this batch on the next of two layer streams
-        (``encoder.layer_stream``), ordered after the producers of the features, poses, graph arrays
-        and weights (readiness events), the caller's stream joining it after: consecutive batches
-        alternate streams, so one batch's encoder runs beside the previous batch's aggregation.  None:
-        not taken (small encoders, stream capture, a shape without a weight image)."""
-        pose = g.edata["pose"]
-        if pose.requires_grad and torch.is_grad_enabled():
-            return None
-        enc = self.edge_encoder.layers
-        ops = encoder_operands(pose, enc[0], enc[2])
-        if ops is None:
-            return None
-        reads, img, _b2, C, _Cp = ops
-        dev = x.device
-        csr = g.csr(dev)
-        graph_reads = tuple((t, t) for t in (csr.indptr, csr.src, csr.eid, csr.graph_off) if t is not None)
-        reads = reads + ((x, x),) + graph_reads
-        s = layer_stream(dev)
-        if enc_begin(dev, pose.shape[0] * C, reads, img, side=s) is None:
-            return None
-        z = launch_encoder(ops, s)
-        if z is None:
-            return None
-        with torch.cuda.stream(s):
-            out = film_mean(x, z, csr, "film_mean", logits=True)
-        enc_end(dev, s, (out,), reads + ((None, img), (z, z)))
-        return out
 
     def forward_cat(self, g, feats: torch.Tensor = None) -> torch.Tensor:
         """``torch.cat((feats, self(g, feats)), 1)`` (``models.py:181-182``) with the aggregate written

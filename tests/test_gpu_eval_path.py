@@ -164,9 +164,8 @@ def _forward(gcn, g, x, own_stream):
 
 
 def test_encoder_stream_ordered_after_input_writes(cuda_device):
-    """The inference encoder runs on its own stream (``encoder.set_encoder_stream``, the default) — the
-    whole no-grad layer on alternating layer streams — ordered after the producers of what it reads,
-    not after everything queued before it.  Its results are the
+    """The inference encoder runs on its own stream (``encoder.set_encoder_stream``, the default), ordered
+    after the producers of what it reads, not after everything queued before it.  Its results are the
     caller's-stream results bit for bit; in-place writes to the poses and to the weights (an optimizer
     step), queued behind long kernels on the caller's stream, are seen by the next forward; and under
     stream capture the layer records on one stream and replays to the same bits."""
@@ -203,13 +202,14 @@ def test_encoder_stream_ordered_after_input_writes(cuda_device):
         gcn.edge_encoder.layers[2].bias.add_(0.5)
     e = _forward(gcn, g, x, True)
     assert torch.equal(e, _forward(gcn, g, x, False)) and not torch.equal(e, d)
-    # the features written in place behind the stall (the whole layer runs on a layer stream)
+    # the features written in place behind the stall
     with torch.no_grad():
         stall()
         x.mul_(1.5)
     f = _forward(gcn, g, x, True)
     assert torch.equal(f, _forward(gcn, g, x, False)) and not torch.equal(f, e)
-    # consecutive calls alternate layer streams: a batch of results, each as on the caller's stream
+    # back-to-back calls (each encoder running ahead beside the previous aggregation), each as on the
+    # caller's stream
     with torch.no_grad():
         runs = [gcn(g, x * (1.0 + 0.1 * i)) for i in range(4)]
         refs = []

@@ -27,12 +27,11 @@ with torch.no_grad():
         for _ in range(20):
             gcn(g, x)
         torch.cuda.synchronize()
-    # (own stream, priority, device-scope join); the last: whole layers on alternating layer streams
-    settings = [(False, 0, True), (True, -1, False), (True, -1, True), ("layer", -1, True)]
+    # (own stream, priority, device-scope join)
+    settings = [(False, 0, True), (True, 0, False), (True, -1, False), (True, 0, True), (True, -1, True)]
     for rnd in range(rounds):
         for on, prio, fj in settings:
-            mrp.encoder.set_encoder_stream(bool(on))
-            mrp.encoder.set_layer_overlap(on == "layer")
+            mrp.encoder.set_encoder_stream(on)
             mrp.encoder.set_encoder_stream_priority(prio)
             mrp.encoder.set_fast_join(fj)
             for _ in range(10):
@@ -45,11 +44,9 @@ with torch.no_grad():
             res.setdefault((on, prio, fj), []).append((time.perf_counter() - t) / steps * 1e6)
             outs[(on, prio, fj)] = out.clone()
 mrp.encoder.set_encoder_stream(True)
-mrp.encoder.set_layer_overlap(True)
 mrp.encoder.set_encoder_stream_priority(-1)
 mrp.encoder.set_fast_join(True)
 for (on, prio, fj), ts in res.items():
-    where = "layer streams" if on == "layer" else ("own" if on else "caller")
-    print(f"encoder stream {where} priority {prio} join {'device' if fj else 'torch'}: "
+    print(f"encoder stream {'own' if on else 'caller'} priority {prio} join {'device' if fj else 'torch'}: "
           + " ".join(f"{t:6.1f}" for t in ts) + f"  min {min(ts):6.1f} us/step", flush=True)
 print("outputs bit-identical:", all(torch.equal(o, outs[settings[0]]) for o in outs.values()))
