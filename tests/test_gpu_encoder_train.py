@@ -180,6 +180,19 @@ def test_split_training_encoder_property(cuda_device, e32, c32, form):
         m.encoder.set_fused_backward(True)
 
 
+@_prop_settings()
+@given(st.integers(1, 1500), st.integers(1, 700), st.sampled_from(["fused", "two_stream", "pose_grad"]))
+def test_padded_training_encoder_property(cuda_device, E, C, form):
+    """Property form of the padded path: any E and C (``EdgeEncoderPaddedFunction`` where either is not
+    a multiple of 32, the split path where both are), every backward form, against float64."""
+    path = "split_train" if E % 32 == 0 and C % 32 == 0 else "split_padded"
+    m.encoder.set_fused_backward(form != "two_stream")
+    try:
+        _check_training_encoder(cuda_device, E, C, pose_grad=form == "pose_grad", path=path)
+    finally:
+        m.encoder.set_fused_backward(True)
+
+
 @pytest.mark.parametrize("E,C", [(1792, 512), (448, 2048), (96, 64)])
 def test_fused_backward_w2t_image_bit_identical(cuda_device, E, C):
     """The fused backward with both products' A operands pre-split (knob enc_bwd_psa 2, the default:
